@@ -1,0 +1,158 @@
+/*
+ * mdx.h -- C-ABI of the MI355X-native motion-detection hot path.
+ *
+ * Drop-in boundary for the reference's in-process seam
+ *   int OpticalFlowCalculator::calculateOpticalFlow(const cv::Mat& image1,
+ *        const cv::Mat& image2, cv::Mat& optical_flow_vectors, int pixel_step,
+ *        cv::Mat& comp, double min_vector_size)
+ * declared at reference common/include/motion_detection/optical_flow_calculator.h:19 and
+ * defined at common/src/optical_flow_calculator.cpp:30-130, called from
+ * MotionDetectionNode::runOpticalFlow (ros/src/motion_detection_node.cpp:76-92, call :82).
+ *
+ * Plain C types only: pointers + sizes, no torch / OpenCV / HIP types in signatures.
+ * Errors are integer codes; no C++ exception crosses this boundary.  A context owns one
+ * HIP stream on one device; it is not thread-safe, but different contexts may be driven
+ * concurrently from different host threads (one context per camera stream / GPU).
+ */
+#ifndef MDX_H_
+#define MDX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDX_ABI_VERSION 1
+
+/* Return codes */
+#define MDX_OK           0
+#define MDX_EINVAL      -1   /* bad argument (size, format, unsupported parameter) */
+#define MDX_EHIP        -2   /* HIP runtime error (message in mdx_last_error) */
+#define MDX_ENOMEM      -3   /* device allocation failed */
+#define MDX_EDEGENERATE  1   /* success, but fewer than 4 accepted vectors: no fit, mask zeroed.
+                                num_vectors == 0 is the reference's "no mask" branch
+                                (optical_flow_calculator.cpp:118); 1..3 is reference UB (:120,
+                                reads past src_points) and is defined here as "no fit". */
+
+/* Pixel formats of the input frames (sensor_msgs/Image encodings the node accepts). */
+#define MDX_FMT_GRAY8 0      /* mono8: cv_bridge rgb8 replication then BGR2GRAY == identity */
+#define MDX_FMT_RGB8  1      /* rgb8 (node.cpp:271), BGR2GRAY weights land swapped (:50) */
+#define MDX_FMT_BGR8  2      /* bgr8: cv_bridge converts to rgb8 first, same swapped weights */
+
+/* Global-motion fit used for the back-warp. */
+#define MDX_FIT_FIRST4   0   /* reference: getPerspectiveTransform on the first 4 accepted
+                                vectors in x-major grid order (:120) */
+#define MDX_FIT_EXTERNAL 1   /* caller supplies H (forward, frame1 -> frame2) per pair */
+
+typedef struct {
+    int    win;              /* LK window side; reference hard-codes 40 (:41). Only 40 is supported. */
+    int    max_level;        /* reference MAX_LEVEL = 5 (:40) */
+    int    max_iters;        /* TermCriteria count = 10 (:44) */
+    double eps;              /* TermCriteria epsilon = 0.03 (:44) */
+    float  min_eig;          /* minEigThreshold = 1e-3 (:71) */
+    int    thresh;           /* threshold(comp, comp, 190, 255, BINARY) (:127) */
+    int    pixel_step;       /* ROS param pixel_step (node.cpp:29; 10 in bag.launch:27) */
+    double min_vector_size;  /* ROS param min_vector_size, default 1.0 (node.cpp:44) */
+    int    fit_mode;         /* MDX_FIT_FIRST4 (default) or MDX_FIT_EXTERNAL */
+} mdx_params;
+
+typedef struct mdx_ctx mdx_ctx;
+
+/* Fill params with the reference's constants. */
+void mdx_default_params(mdx_params* p);
+
+/* Number of grid points for a frame: ceil(w/ps) * ceil(h/ps) (:56-64, x-major order:
+ * point k = ix*ny + iy sits at (ix*ps, iy*ps)). */
+int mdx_grid_count(int w, int h, int pixel_step);
+
+/* Create a context on HIP device `device`.  max_w/max_h/max_batch size the device
+ * workspace (pyramids, derivatives, scratch) so that the per-frame path never allocates.
+ * Returns NULL on failure; mdx_create_error() then holds the reason. */
+mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, const mdx_params* p);
+const char* mdx_create_error(void);
+int mdx_destroy(mdx_ctx* ctx);
+const char* mdx_last_error(const mdx_ctx* ctx);
+int mdx_set_params(mdx_ctx* ctx, const mdx_params* p);
+int mdx_get_params(const mdx_ctx* ctx, mdx_params* p);
+
+/* The context's HIP stream (hipStream_t as void*) and device id; for interop only. */
+void* mdx_stream(mdx_ctx* ctx);
+int mdx_device(const mdx_ctx* ctx);
+int mdx_sync(mdx_ctx* ctx);
+
+/*
+ * Synchronous host-buffer entry: the direct replacement of calculateOpticalFlow.
+ *   img1, img2  w x h frames, row pitch `stride` bytes, format `fmt`.
+ *   next_pts    [2*npts] float  LK output positions (x-major grid order)        or NULL
+ *   status      [npts]   uint8  LK status                                       or NULL
+ *   vectors     [4*npts] double the reference's Vec4d per grid point:
+ *               (x, y, dx, dy) accepted / (x, y, 0, 0) tracked / (-1, -1, 0, 0) lost
+ *               (:78-117; stored densely per grid point)     or NULL
+ *   mask        [w*h]    uint8  thresholded |warp(gray1) - gray2| (comp, :122-127) or NULL
+ *   H           [9]      double perspective transform (first-4 fit or external)  or NULL
+ *   H_external  [9]      double forward H when fit_mode == MDX_FIT_EXTERNAL, else NULL
+ *   num_vectors          number of accepted vectors (the reference's return value)
+ * Returns MDX_OK, MDX_EDEGENERATE, or a negative error.
+ */
+int mdx_flow_warp_diff(mdx_ctx* ctx, const uint8_t* img1, const uint8_t* img2,
+                       int w, int h, int stride, int fmt,
+                       float* next_pts, uint8_t* status, double* vectors,
+                       uint8_t* mask, double* H, const double* H_external, int* num_vectors);
+
+/*
+ * Asynchronous batched device entry (zero-copy; everything stays in HBM).  Pair i reads
+ * d_img1 + i*frame_stride and d_img2 + i*frame_stride.  Outputs (device pointers, each may
+ * be NULL except where noted):
+ *   d_next_pts  [batch][npts][2] float     d_status [batch][npts] uint8
+ *   d_vectors   [batch][npts][4] double    d_mask   [batch][h][w] uint8
+ *   d_H         [batch][9] double          d_num_vectors [batch] int32
+ *   d_H_external[batch][9] double (input; required iff fit_mode == MDX_FIT_EXTERNAL)
+ * Work is enqueued on the context stream; call mdx_sync (or sync the stream) before use.
+ */
+int mdx_flow_warp_diff_batch_dev(mdx_ctx* ctx, int batch,
+                                 const uint8_t* d_img1, const uint8_t* d_img2,
+                                 int w, int h, int stride, size_t frame_stride, int fmt,
+                                 float* d_next_pts, uint8_t* d_status, double* d_vectors,
+                                 uint8_t* d_mask, double* d_H, const double* d_H_external,
+                                 int* d_num_vectors);
+
+/*
+ * The fused back-warp + absdiff + threshold kernel alone (rows A8-A10): for each pair,
+ * mask = (|warpPerspective(gray1, H) - gray2| > thresh) * 255 with the reference's
+ * warpPerspective arithmetic (inverse of H, FP64 coordinates, 1/32 px, BORDER_CONSTANT 0).
+ * d_gray1/d_gray2: [batch] frames of w x h gray8, row pitch `stride`, frame pitch
+ * `frame_stride`.  d_H: [batch][9] forward transforms (device).  d_mask: [batch][h][w].
+ */
+int mdx_warp_diff_dev(mdx_ctx* ctx, int batch, const uint8_t* d_gray1, const uint8_t* d_gray2,
+                      int w, int h, int stride, size_t frame_stride,
+                      const double* d_H, uint8_t* d_mask);
+
+/* Device memory helpers so hosts without a HIP toolchain (ctypes, cgo, JNI) can stage
+ * buffers: allocation on the context's device, copies ordered on its stream. */
+void* mdx_dev_alloc(mdx_ctx* ctx, size_t bytes);
+int mdx_dev_free(mdx_ctx* ctx, void* p);
+int mdx_memcpy_h2d(mdx_ctx* ctx, void* dst, const void* src, size_t bytes);
+int mdx_memcpy_d2h(mdx_ctx* ctx, void* dst, const void* src, size_t bytes);
+
+/* Timing of the most recent batched call, per stage, from HIP events on the ctx stream
+ * (milliseconds). stage: 0 gray+pad, 1 pyramids, 2 Scharr, 3 LK, 4 classify+fit,
+ * 5 warp+diff, 6 total.  Enabled by mdx_enable_timing(ctx, 1). */
+int mdx_enable_timing(mdx_ctx* ctx, int on);
+int mdx_stage_ms(mdx_ctx* ctx, int stage, float* ms);
+
+/*
+ * Synthetic frame-pair generator used by the benchmark and tests (host, deterministic,
+ * byte-identical on every x86-64 host).  Spec in DESIGN.md §5: blurred value noise +
+ * rectangles; frame 2 = frame 1 under the affine H_true (0.5 deg rotation about the
+ * centre, scale 1.01, translation (3.2, -1.7)) + one moving patch (+8, +5) + +-2 LSB noise.
+ * channels = 1 (gray) or 3 (rgb8).  H_true (9 doubles, forward) is written if non-NULL.
+ */
+int mdx_synth_pair(uint64_t seed, int w, int h, int channels, uint8_t* img1, uint8_t* img2,
+                   double* H_true, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MDX_H_ */

@@ -1,0 +1,120 @@
+"""ctypes binding of libmdx.so (the C-ABI declared in include/mdx.h).
+
+The library is built in-tree (motion_detection_amd/lib/libmdx.so) by
+``motion_detection_amd.build()`` / ``__graft_entry__.build()``.  There is no CPU or
+PyTorch fallback: if the library is missing, importing the compute API raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmdx.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+MDX_OK = 0
+MDX_EINVAL = -1
+MDX_EHIP = -2
+MDX_ENOMEM = -3
+MDX_EDEGENERATE = 1
+
+FMT_GRAY8, FMT_RGB8, FMT_BGR8 = 0, 1, 2
+FIT_FIRST4, FIT_EXTERNAL = 0, 1
+
+# every symbol include/mdx.h declares (checked by tests/test_abi.py)
+EXPORTED = [
+    "mdx_default_params", "mdx_grid_count", "mdx_create", "mdx_create_error", "mdx_destroy",
+    "mdx_last_error", "mdx_set_params", "mdx_get_params", "mdx_stream", "mdx_device", "mdx_sync",
+    "mdx_flow_warp_diff", "mdx_flow_warp_diff_batch_dev", "mdx_warp_diff_dev", "mdx_dev_alloc",
+    "mdx_dev_free", "mdx_memcpy_h2d", "mdx_memcpy_d2h", "mdx_enable_timing", "mdx_stage_ms",
+    "mdx_synth_pair",
+]
+
+
+class MdxParams(C.Structure):
+    _fields_ = [("win", C.c_int), ("max_level", C.c_int), ("max_iters", C.c_int), ("eps", C.c_double),
+                ("min_eig", C.c_float), ("thresh", C.c_int), ("pixel_step", C.c_int),
+                ("min_vector_size", C.c_double), ("fit_mode", C.c_int)]
+
+
+class MdxError(RuntimeError):
+    """Raised for every negative return code of the C-ABI."""
+
+
+def build(force: bool = False) -> str:
+    """Compile libmdx.so for gfx950 with hipcc (csrc/Makefile)."""
+    cmd = ["make", "-s", "-C", CSRC] + (["-B"] if force else [])
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MdxError(f"{LIB_PATH} is missing: build it with motion_detection_amd.build() "
+                       "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    vp, u8p, f32p, f64p, i32p = C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p
+    L.mdx_default_params.argtypes = [C.POINTER(MdxParams)]
+    L.mdx_default_params.restype = None
+    L.mdx_grid_count.argtypes = [C.c_int, C.c_int, C.c_int]
+    L.mdx_grid_count.restype = C.c_int
+    L.mdx_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(MdxParams)]
+    L.mdx_create.restype = vp
+    L.mdx_create_error.argtypes = []
+    L.mdx_create_error.restype = C.c_char_p
+    L.mdx_destroy.argtypes = [vp]
+    L.mdx_destroy.restype = C.c_int
+    L.mdx_last_error.argtypes = [vp]
+    L.mdx_last_error.restype = C.c_char_p
+    L.mdx_set_params.argtypes = [vp, C.POINTER(MdxParams)]
+    L.mdx_set_params.restype = C.c_int
+    L.mdx_get_params.argtypes = [vp, C.POINTER(MdxParams)]
+    L.mdx_get_params.restype = C.c_int
+    L.mdx_stream.argtypes = [vp]
+    L.mdx_stream.restype = vp
+    L.mdx_device.argtypes = [vp]
+    L.mdx_device.restype = C.c_int
+    L.mdx_sync.argtypes = [vp]
+    L.mdx_sync.restype = C.c_int
+    L.mdx_flow_warp_diff.argtypes = [vp, u8p, u8p, C.c_int, C.c_int, C.c_int, C.c_int, f32p, u8p, f64p, u8p,
+                                     f64p, f64p, C.POINTER(C.c_int)]
+    L.mdx_flow_warp_diff.restype = C.c_int
+    L.mdx_flow_warp_diff_batch_dev.argtypes = [vp, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int, C.c_size_t, C.c_int,
+                                               vp, vp, vp, vp, vp, vp, vp]
+    L.mdx_flow_warp_diff_batch_dev.restype = C.c_int
+    L.mdx_warp_diff_dev.argtypes = [vp, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int, C.c_size_t, vp, vp]
+    L.mdx_warp_diff_dev.restype = C.c_int
+    L.mdx_dev_alloc.argtypes = [vp, C.c_size_t]
+    L.mdx_dev_alloc.restype = vp
+    L.mdx_dev_free.argtypes = [vp, vp]
+    L.mdx_dev_free.restype = C.c_int
+    L.mdx_memcpy_h2d.argtypes = [vp, vp, vp, C.c_size_t]
+    L.mdx_memcpy_h2d.restype = C.c_int
+    L.mdx_memcpy_d2h.argtypes = [vp, vp, vp, C.c_size_t]
+    L.mdx_memcpy_d2h.restype = C.c_int
+    L.mdx_enable_timing.argtypes = [vp, C.c_int]
+    L.mdx_enable_timing.restype = C.c_int
+    L.mdx_stage_ms.argtypes = [vp, C.c_int, C.POINTER(C.c_float)]
+    L.mdx_stage_ms.restype = C.c_int
+    L.mdx_synth_pair.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, u8p, u8p, f64p, C.c_int]
+    L.mdx_synth_pair.restype = C.c_int
+    _lib = L
+    return L
+
+
+def default_params(**overrides) -> MdxParams:
+    p = MdxParams()
+    lib().mdx_default_params(C.byref(p))
+    for k, v in overrides.items():
+        if not hasattr(p, k):
+            raise TypeError(f"unknown parameter {k!r}")
+        setattr(p, k, v)
+    return p

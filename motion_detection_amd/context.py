@@ -1,0 +1,175 @@
+"""Python host over the C-ABI: a device context per camera stream / GPU.
+
+Thin ownership wrapper around ``mdx_ctx`` (include/mdx.h).  Numpy arrays on the host
+side, raw device pointers (ints) for the zero-copy batched entry; no torch types.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import MdxError, lib
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def grid_count(w: int, h: int, pixel_step: int) -> int:
+    return lib().mdx_grid_count(w, h, pixel_step)
+
+
+def grid_points(w: int, h: int, pixel_step: int) -> np.ndarray:
+    """Grid of the reference (optical_flow_calculator.cpp:56-64): x-major, float32 (n, 2)."""
+    xs = np.arange(0, w, pixel_step, dtype=np.float32)
+    ys = np.arange(0, h, pixel_step, dtype=np.float32)
+    gx, gy = np.meshgrid(xs, ys, indexing="ij")
+    return np.stack([gx.ravel(), gy.ravel()], 1)
+
+
+@dataclass
+class FlowResult:
+    num_vectors: int        # reference return value
+    next_pts: np.ndarray    # (npts, 2) float32, LK output positions, x-major grid order
+    status: np.ndarray      # (npts,) uint8
+    vectors: np.ndarray     # (npts, 4) float64: (x, y, dx, dy) / (x, y, 0, 0) / (-1, -1, 0, 0)
+    mask: np.ndarray | None  # (h, w) uint8 or None
+    H: np.ndarray           # (3, 3) float64 (zeros when no fit)
+    code: int               # MDX_OK or MDX_EDEGENERATE
+
+
+class Context:
+    """One device context (mdx_ctx): workspace sized at creation, one HIP stream."""
+
+    def __init__(self, device: int = 0, max_w: int = 1920, max_h: int = 1080, max_batch: int = 1, **params):
+        self._p = _lib.default_params(**params)
+        h = lib().mdx_create(device, max_w, max_h, max_batch, C.byref(self._p))
+        if not h:
+            raise MdxError("mdx_create failed: " + lib().mdx_create_error().decode())
+        self._h = C.c_void_p(h)
+
+    # -- lifetime
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mdx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int) -> int:
+        if rc < 0:
+            raise MdxError(f"mdx error {rc}: {lib().mdx_last_error(self._h).decode()}")
+        return rc
+
+    # -- params
+    @property
+    def params(self) -> _lib.MdxParams:
+        p = _lib.MdxParams()
+        self._check(lib().mdx_get_params(self._h, C.byref(p)))
+        return p
+
+    def set_params(self, **kw):
+        p = self.params
+        for k, v in kw.items():
+            setattr(p, k, v)
+        self._check(lib().mdx_set_params(self._h, C.byref(p)))
+
+    # -- host entry (drop-in for calculateOpticalFlow)
+    def flow_warp_diff(self, img1: np.ndarray, img2: np.ndarray, fmt: int | None = None, want_mask: bool = True,
+                       H_external: np.ndarray | None = None) -> FlowResult:
+        img1 = np.ascontiguousarray(img1, dtype=np.uint8)
+        img2 = np.ascontiguousarray(img2, dtype=np.uint8)
+        if img1.shape != img2.shape:
+            raise ValueError("frames must have the same shape")
+        h, w = img1.shape[:2]
+        if fmt is None:
+            fmt = _lib.FMT_GRAY8 if img1.ndim == 2 else _lib.FMT_RGB8
+        p = self.params
+        n = grid_count(w, h, p.pixel_step)
+        nextp = np.zeros((n, 2), np.float32)
+        status = np.zeros(n, np.uint8)
+        vec = np.zeros((n, 4), np.float64)
+        mask = np.zeros((h, w), np.uint8) if want_mask else None
+        H = np.zeros(9, np.float64)
+        Hx = None if H_external is None else np.ascontiguousarray(H_external, dtype=np.float64).ravel()
+        num = C.c_int(0)
+        rc = self._check(lib().mdx_flow_warp_diff(self._h, _ptr(img1), _ptr(img2), w, h, img1.strides[0], fmt,
+                                                  _ptr(nextp), _ptr(status), _ptr(vec), _ptr(mask), _ptr(H), _ptr(Hx),
+                                                  C.byref(num)))
+        return FlowResult(num.value, nextp, status, vec, mask, H.reshape(3, 3), rc)
+
+    # -- device entries (pointers are ints, e.g. torch.Tensor.data_ptr())
+    def flow_warp_diff_batch_dev(self, batch: int, d_img1: int, d_img2: int, w: int, h: int, stride: int,
+                                 frame_stride: int, fmt: int = _lib.FMT_GRAY8, d_next_pts: int = 0, d_status: int = 0,
+                                 d_vectors: int = 0, d_mask: int = 0, d_H: int = 0, d_H_external: int = 0,
+                                 d_num_vectors: int = 0) -> int:
+        v = lambda x: C.c_void_p(x) if x else None  # noqa: E731
+        return self._check(lib().mdx_flow_warp_diff_batch_dev(
+            self._h, batch, v(d_img1), v(d_img2), w, h, stride, frame_stride, fmt, v(d_next_pts), v(d_status),
+            v(d_vectors), v(d_mask), v(d_H), v(d_H_external), v(d_num_vectors)))
+
+    def warp_diff_dev(self, batch: int, d_gray1: int, d_gray2: int, w: int, h: int, stride: int, frame_stride: int,
+                      d_H: int, d_mask: int) -> int:
+        return self._check(lib().mdx_warp_diff_dev(self._h, batch, C.c_void_p(d_gray1), C.c_void_p(d_gray2), w, h,
+                                                   stride, frame_stride, C.c_void_p(d_H), C.c_void_p(d_mask)))
+
+    def sync(self):
+        self._check(lib().mdx_sync(self._h))
+
+    @property
+    def stream(self) -> int:
+        return lib().mdx_stream(self._h) or 0
+
+    def enable_timing(self, on: bool = True):
+        self._check(lib().mdx_enable_timing(self._h, int(on)))
+
+    def stage_ms(self) -> dict:
+        names = ["gray_pad", "pyrdown", "scharr", "lk", "classify_fit", "warp_diff", "total"]
+        out = {}
+        for i, nm in enumerate(names):
+            ms = C.c_float(0)
+            self._check(lib().mdx_stage_ms(self._h, i, C.byref(ms)))
+            out[nm] = ms.value
+        return out
+
+    # -- device memory helpers (no torch needed)
+    def dev_alloc(self, nbytes: int) -> int:
+        p = lib().mdx_dev_alloc(self._h, nbytes)
+        if not p:
+            raise MdxError(lib().mdx_last_error(self._h).decode())
+        return p
+
+    def dev_free(self, ptr: int):
+        self._check(lib().mdx_dev_free(self._h, C.c_void_p(ptr)))
+
+    def h2d(self, dst: int, src: np.ndarray):
+        src = np.ascontiguousarray(src)
+        self._check(lib().mdx_memcpy_h2d(self._h, C.c_void_p(dst), _ptr(src), src.nbytes))
+
+    def d2h(self, dst: np.ndarray, src: int):
+        self._check(lib().mdx_memcpy_d2h(self._h, _ptr(dst), C.c_void_p(src), dst.nbytes))
+
+
+def synth_pair(seed: int, w: int, h: int, channels: int = 1, nthreads: int = 0):
+    """Deterministic synthetic frame pair.  Returns (img1, img2, H_true)."""
+    shape = (h, w) if channels == 1 else (h, w, channels)
+    a = np.empty(shape, np.uint8)
+    b = np.empty(shape, np.uint8)
+    H = np.zeros(9, np.float64)
+    rc = lib().mdx_synth_pair(seed, w, h, channels, _ptr(a), _ptr(b), _ptr(H), nthreads)
+    if rc != 0:
+        raise MdxError(f"mdx_synth_pair failed ({rc})")
+    return a, b, H.reshape(3, 3)

@@ -1,0 +1,434 @@
+// mdx_api.cpp -- host side of the C-ABI (include/mdx.h): context, device workspace sized
+// once at create time, and the per-call pipeline
+//   gray+pad -> pyrDown x L (both frames) -> Scharr x (L+1) -> LK -> classify+fit -> warp+diff
+// enqueued on the context's HIP stream.  Replaces OpticalFlowCalculator::calculateOpticalFlow
+// (reference common/src/optical_flow_calculator.cpp:30-130); no allocation on the per-frame
+// path once the workspace fits the frame size.
+#include "../../include/mdx.h"
+#include "mdx_internal.h"
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+using namespace mdx;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct mdx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    mdx_params prm{};
+    int max_w = 0, max_h = 0, max_batch = 0;
+    DevBuf pyr1, pyr2, der, fits;            // pyramid / derivative / fit workspace
+    DevBuf in1, in2, np, st, vec, mask, H, Hext, num;   // host-path staging
+    DevBuf bnp, bst;                         // LK outputs the batched caller did not ask for
+    bool timing = false;
+    hipEvent_t ev[8] = {};
+    std::string err;
+};
+
+static thread_local std::string g_create_err;
+
+static int set_err(mdx_ctx* c, int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define HIP_OR_RETURN(c, expr)                                                                 \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return set_err((c), MDX_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));      \
+    } while (0)
+
+extern "C" void mdx_default_params(mdx_params* p)
+{
+    p->win = 40;
+    p->max_level = 5;
+    p->max_iters = 10;
+    p->eps = 0.03;
+    p->min_eig = 0.001f;
+    p->thresh = 190;
+    p->pixel_step = 10;
+    p->min_vector_size = 1.0;
+    p->fit_mode = MDX_FIT_FIRST4;
+}
+
+extern "C" int mdx_grid_count(int w, int h, int ps)
+{
+    if (w <= 0 || h <= 0 || ps <= 0) return 0;
+    return ((w + ps - 1) / ps) * ((h + ps - 1) / ps);
+}
+
+static int check_params(const mdx_params* p, std::string* why)
+{
+    if (p->win != kWin) { *why = "only win == 40 (the reference constant) is supported"; return 0; }
+    if (p->max_level < 0 || p->max_level >= kMaxLevels) { *why = "max_level out of range [0, 7]"; return 0; }
+    if (p->pixel_step <= 0) { *why = "pixel_step must be > 0 (reference leaves it unset: UB)"; return 0; }
+    if (p->fit_mode != MDX_FIT_FIRST4 && p->fit_mode != MDX_FIT_EXTERNAL) { *why = "bad fit_mode"; return 0; }
+    return 1;
+}
+
+// buildOpticalFlowPyramid level count and the padded slab layout for a w x h frame.
+static Geometry make_geometry(int w, int h, int max_level)
+{
+    Geometry g{};
+    int sw = w, sh = h;
+    long long img = 0, der = 0;
+    int lvl;
+    for (lvl = 0; lvl <= max_level; lvl++) {
+        Level& L = g.lv[lvl];
+        L.w = sw;
+        L.h = sh;
+        L.pitch = (kXOff + sw + kPad + 63) / 64 * 64;
+        L.rows = kPad + sh + kPad;
+        L.img_off = img;
+        L.der_off = der;
+        img += (long long)L.pitch * L.rows;
+        der += (long long)L.pitch * L.rows;
+        g.nlev = lvl + 1;
+        sw = (sw + 1) / 2;
+        sh = (sh + 1) / 2;
+        if (sw <= kWin || sh <= kWin) break;
+    }
+    g.img_bytes = (img + 255) / 256 * 256;
+    g.der_words = (der + 63) / 64 * 64;
+    return g;
+}
+
+static int ensure(mdx_ctx* c, DevBuf& b, size_t need)
+{
+    if (need == 0) need = 1;
+    if (b.p && b.cap >= need) return MDX_OK;
+    if (b.p) {
+        hipStreamSynchronize(c->stream);
+        hipFree(b.p);
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    if (hipMalloc(&b.p, need) != hipSuccess) {
+        b.p = nullptr;
+        return set_err(c, MDX_ENOMEM, "hipMalloc(%zu) failed", need);
+    }
+    b.cap = need;
+    return MDX_OK;
+}
+
+static int ensure_workspace(mdx_ctx* c, const Geometry& g, int batch)
+{
+    int rc;
+    if ((rc = ensure(c, c->pyr1, (size_t)g.img_bytes * batch)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->pyr2, (size_t)g.img_bytes * batch)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->der, (size_t)g.der_words * 4 * batch)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->fits, sizeof(PairFit) * (size_t)batch)) != MDX_OK) return rc;
+    return MDX_OK;
+}
+
+extern "C" const char* mdx_create_error(void) { return g_create_err.c_str(); }
+
+extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, const mdx_params* p)
+{
+    g_create_err.clear();
+    mdx_params prm;
+    if (p) prm = *p;
+    else mdx_default_params(&prm);
+    std::string why;
+    if (!check_params(&prm, &why)) { g_create_err = why; return nullptr; }
+    if (max_w <= 0 || max_h <= 0 || max_batch <= 0) { g_create_err = "max_w/max_h/max_batch must be > 0"; return nullptr; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { g_create_err = "no HIP device visible"; return nullptr; }
+    if (device < 0 || device >= ndev) { g_create_err = "device index out of range"; return nullptr; }
+    if (hipSetDevice(device) != hipSuccess) { g_create_err = "hipSetDevice failed"; return nullptr; }
+    mdx_ctx* c = new mdx_ctx();
+    c->device = device;
+    c->prm = prm;
+    c->max_w = max_w;
+    c->max_h = max_h;
+    c->max_batch = max_batch;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        g_create_err = "hipStreamCreate failed";
+        delete c;
+        return nullptr;
+    }
+    for (auto& e : c->ev) hipEventCreate(&e);
+    Geometry g = make_geometry(max_w, max_h, prm.max_level);
+    if (ensure_workspace(c, g, max_batch) != MDX_OK) {
+        g_create_err = c->err;
+        mdx_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+extern "C" int mdx_destroy(mdx_ctx* c)
+{
+    if (!c) return MDX_EINVAL;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    DevBuf* bufs[] = {&c->pyr1, &c->pyr2, &c->der, &c->fits, &c->in1, &c->in2, &c->np, &c->st,
+                      &c->vec, &c->mask, &c->H, &c->Hext, &c->num, &c->bnp, &c->bst};
+    for (DevBuf* b : bufs)
+        if (b->p) hipFree(b->p);
+    for (auto& e : c->ev)
+        if (e) hipEventDestroy(e);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return MDX_OK;
+}
+
+extern "C" const char* mdx_last_error(const mdx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+extern "C" void* mdx_stream(mdx_ctx* c) { return c ? (void*)c->stream : nullptr; }
+extern "C" int mdx_device(const mdx_ctx* c) { return c ? c->device : -1; }
+
+extern "C" int mdx_set_params(mdx_ctx* c, const mdx_params* p)
+{
+    if (!c || !p) return MDX_EINVAL;
+    std::string why;
+    if (!check_params(p, &why)) return set_err(c, MDX_EINVAL, "%s", why.c_str());
+    c->prm = *p;
+    return MDX_OK;
+}
+
+extern "C" int mdx_get_params(const mdx_ctx* c, mdx_params* p)
+{
+    if (!c || !p) return MDX_EINVAL;
+    *p = c->prm;
+    return MDX_OK;
+}
+
+extern "C" int mdx_sync(mdx_ctx* c)
+{
+    if (!c) return MDX_EINVAL;
+    HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
+    return MDX_OK;
+}
+
+extern "C" int mdx_enable_timing(mdx_ctx* c, int on)
+{
+    if (!c) return MDX_EINVAL;
+    c->timing = on != 0;
+    return MDX_OK;
+}
+
+extern "C" int mdx_stage_ms(mdx_ctx* c, int stage, float* ms)
+{
+    if (!c || !ms || stage < 0 || stage > 6) return MDX_EINVAL;
+    if (!c->timing) return set_err(c, MDX_EINVAL, "timing not enabled");
+    HIP_OR_RETURN(c, hipEventSynchronize(c->ev[6]));
+    if (stage == 6) HIP_OR_RETURN(c, hipEventElapsedTime(ms, c->ev[0], c->ev[6]));
+    else HIP_OR_RETURN(c, hipEventElapsedTime(ms, c->ev[stage], c->ev[stage + 1]));
+    return MDX_OK;
+}
+
+static inline void mark(mdx_ctx* c, int i)
+{
+    if (c->timing) hipEventRecord(c->ev[i], c->stream);
+}
+
+// The pipeline on device buffers.  d_np/d_st must be valid (LK writes them).
+static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint8_t* d_img2, int w, int h, int stride,
+                        size_t frame_stride, int fmt, float* d_np, uint8_t* d_st, double* d_vec, uint8_t* d_mask,
+                        double* d_H, const double* d_Hext, int* d_num)
+{
+    const mdx_params& P = c->prm;
+    if (w <= 0 || h <= 0 || batch <= 0) return set_err(c, MDX_EINVAL, "bad frame size or batch");
+    if (fmt < MDX_FMT_GRAY8 || fmt > MDX_FMT_BGR8) return set_err(c, MDX_EINVAL, "bad pixel format %d", fmt);
+    const int cn = fmt == MDX_FMT_GRAY8 ? 1 : 3;
+    if (stride < w * cn) return set_err(c, MDX_EINVAL, "stride %d < w*channels %d", stride, w * cn);
+    if (batch > 1 && frame_stride < (size_t)stride * h) return set_err(c, MDX_EINVAL, "frame_stride too small");
+    if (P.fit_mode == MDX_FIT_EXTERNAL && !d_Hext) return set_err(c, MDX_EINVAL, "fit_mode EXTERNAL needs H_external");
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    Geometry g = make_geometry(w, h, P.max_level);
+    int rc = ensure_workspace(c, g, batch);
+    if (rc != MDX_OK) return rc;
+    const int npts = mdx_grid_count(w, h, P.pixel_step);
+    const int ny = (h + P.pixel_step - 1) / P.pixel_step;
+    hipStream_t s = c->stream;
+    uint8_t* pyr1 = c->pyr1.as<uint8_t>();
+    uint8_t* pyr2 = c->pyr2.as<uint8_t>();
+    uint32_t* der = c->der.as<uint32_t>();
+    PairFit* fits = c->fits.as<PairFit>();
+
+    mark(c, 0);
+    HIP_OR_RETURN(c, launch_gray_pad(s, batch, d_img1, d_img2, w, h, stride, (long long)frame_stride, fmt, pyr1, pyr2, g));
+    mark(c, 1);
+    for (int l = 1; l < g.nlev; l++) HIP_OR_RETURN(c, launch_pyrdown(s, batch, pyr1, pyr2, g, l));
+    mark(c, 2);
+    for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, batch, pyr1, der, g, l));
+    mark(c, 3);
+    if (npts > 0) {
+        LkArgs a{};
+        a.pyr1 = pyr1;
+        a.pyr2 = pyr2;
+        a.der = der;
+        a.g = g;
+        a.maxl = g.nlev - 1;
+        a.npts = npts;
+        a.ny = ny;
+        a.pixel_step = P.pixel_step;
+        a.max_iters = std::min(std::max(P.max_iters, 0), 100);
+        a.min_eig = P.min_eig;
+        const double e = std::min(std::max(P.eps, 0.), 10.);
+        a.eps2 = e * e;
+        a.next_pts = d_np;
+        a.status = d_st;
+        HIP_OR_RETURN(c, launch_lk(s, batch, a));
+    }
+    mark(c, 4);
+    HIP_OR_RETURN(c, launch_classify_fit(s, batch, d_np, d_st, npts, ny, P.pixel_step, P.min_vector_size, d_vec, fits,
+                                         P.fit_mode, d_Hext));
+    mark(c, 5);
+    if (d_mask) {
+        const Level& L0 = g.lv[0];
+        const uint8_t* g1 = pyr1 + L0.img_off + L0.core();
+        const uint8_t* g2 = pyr2 + L0.img_off + L0.core();
+        HIP_OR_RETURN(c, launch_warp_diff(s, batch, g1, g.img_bytes, L0.pitch, g2, g.img_bytes, L0.pitch, w, h, fits,
+                                          d_mask, (long long)w * h, P.thresh));
+    }
+    if (d_H || d_num) HIP_OR_RETURN(c, launch_export_fit(s, batch, fits, d_H, d_num));
+    mark(c, 6);
+    return MDX_OK;
+}
+
+extern "C" int mdx_flow_warp_diff_batch_dev(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint8_t* d_img2,
+                                            int w, int h, int stride, size_t frame_stride, int fmt, float* d_next_pts,
+                                            uint8_t* d_status, double* d_vectors, uint8_t* d_mask, double* d_H,
+                                            const double* d_H_external, int* d_num_vectors)
+{
+    if (!c) return MDX_EINVAL;
+    if (!d_img1 || !d_img2 || batch <= 0) return set_err(c, MDX_EINVAL, "null frame pointer or batch <= 0");
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    const size_t need = (size_t)mdx_grid_count(w, h, c->prm.pixel_step) * batch;
+    int rc;
+    if (!d_next_pts) {
+        if ((rc = ensure(c, c->bnp, need * 8)) != MDX_OK) return rc;
+        d_next_pts = c->bnp.as<float>();
+    }
+    if (!d_status) {
+        if ((rc = ensure(c, c->bst, need)) != MDX_OK) return rc;
+        d_status = c->bst.as<uint8_t>();
+    }
+    return run_pipeline(c, batch, d_img1, d_img2, w, h, stride, frame_stride, fmt, d_next_pts, d_status, d_vectors,
+                        d_mask, d_H, d_H_external, d_num_vectors);
+}
+
+extern "C" int mdx_flow_warp_diff(mdx_ctx* c, const uint8_t* img1, const uint8_t* img2, int w, int h, int stride,
+                                  int fmt, float* next_pts, uint8_t* status, double* vectors, uint8_t* mask, double* H,
+                                  const double* H_external, int* num_vectors)
+{
+    if (!c) return MDX_EINVAL;
+    if (!img1 || !img2) return set_err(c, MDX_EINVAL, "null frame pointer");
+    if (w <= 0 || h <= 0) return set_err(c, MDX_EINVAL, "bad frame size");
+    if (fmt < MDX_FMT_GRAY8 || fmt > MDX_FMT_BGR8) return set_err(c, MDX_EINVAL, "bad pixel format %d", fmt);
+    const int cn = fmt == MDX_FMT_GRAY8 ? 1 : 3;
+    if (stride < w * cn) return set_err(c, MDX_EINVAL, "stride %d < w*channels %d", stride, w * cn);
+    if (c->prm.fit_mode == MDX_FIT_EXTERNAL && !H_external)
+        return set_err(c, MDX_EINVAL, "fit_mode EXTERNAL needs H_external");
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    const size_t in_bytes = (size_t)stride * h;
+    const int npts = mdx_grid_count(w, h, c->prm.pixel_step);
+    const size_t pts = (size_t)(npts > 0 ? npts : 1);
+    int rc;
+    if ((rc = ensure(c, c->in1, in_bytes)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->in2, in_bytes)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->np, pts * 8)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->st, pts)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->vec, pts * 32)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->mask, (size_t)w * h)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->H, 72)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->Hext, 72)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->num, 4)) != MDX_OK) return rc;
+
+    hipStream_t s = c->stream;
+    HIP_OR_RETURN(c, hipMemcpyAsync(c->in1.p, img1, in_bytes, hipMemcpyHostToDevice, s));
+    HIP_OR_RETURN(c, hipMemcpyAsync(c->in2.p, img2, in_bytes, hipMemcpyHostToDevice, s));
+    if (H_external) HIP_OR_RETURN(c, hipMemcpyAsync(c->Hext.p, H_external, 72, hipMemcpyHostToDevice, s));
+    rc = run_pipeline(c, 1, c->in1.as<uint8_t>(), c->in2.as<uint8_t>(), w, h, stride, in_bytes, fmt, c->np.as<float>(),
+                      c->st.as<uint8_t>(), vectors ? c->vec.as<double>() : nullptr,
+                      mask ? c->mask.as<uint8_t>() : nullptr, c->H.as<double>(),
+                      H_external ? c->Hext.as<double>() : nullptr, c->num.as<int>());
+    if (rc != MDX_OK) return rc;
+    int num = 0;
+    if (next_pts && npts > 0) HIP_OR_RETURN(c, hipMemcpyAsync(next_pts, c->np.p, (size_t)npts * 8, hipMemcpyDeviceToHost, s));
+    if (status && npts > 0) HIP_OR_RETURN(c, hipMemcpyAsync(status, c->st.p, (size_t)npts, hipMemcpyDeviceToHost, s));
+    if (vectors && npts > 0) HIP_OR_RETURN(c, hipMemcpyAsync(vectors, c->vec.p, (size_t)npts * 32, hipMemcpyDeviceToHost, s));
+    if (mask) HIP_OR_RETURN(c, hipMemcpyAsync(mask, c->mask.p, (size_t)w * h, hipMemcpyDeviceToHost, s));
+    if (H) HIP_OR_RETURN(c, hipMemcpyAsync(H, c->H.p, 72, hipMemcpyDeviceToHost, s));
+    HIP_OR_RETURN(c, hipMemcpyAsync(&num, c->num.p, 4, hipMemcpyDeviceToHost, s));
+    HIP_OR_RETURN(c, hipStreamSynchronize(s));
+    if (num_vectors) *num_vectors = num;
+    if (c->prm.fit_mode == MDX_FIT_FIRST4 && num < 4) return MDX_EDEGENERATE;
+    return MDX_OK;
+}
+
+extern "C" int mdx_warp_diff_dev(mdx_ctx* c, int batch, const uint8_t* d_gray1, const uint8_t* d_gray2, int w, int h,
+                                 int stride, size_t frame_stride, const double* d_H, uint8_t* d_mask)
+{
+    if (!c) return MDX_EINVAL;
+    if (!d_gray1 || !d_gray2 || !d_H || !d_mask || batch <= 0 || w <= 0 || h <= 0 || stride < w)
+        return set_err(c, MDX_EINVAL, "mdx_warp_diff_dev: bad argument");
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    int rc = ensure(c, c->fits, sizeof(PairFit) * (size_t)batch);
+    if (rc != MDX_OK) return rc;
+    hipStream_t s = c->stream;
+    PairFit* fits = c->fits.as<PairFit>();
+    mark(c, 0);
+    for (int i = 1; i < 5; i++) mark(c, i);
+    HIP_OR_RETURN(c, launch_set_fit_external(s, batch, d_H, fits));
+    mark(c, 5);
+    HIP_OR_RETURN(c, launch_warp_diff(s, batch, d_gray1, (long long)frame_stride, stride, d_gray2,
+                                      (long long)frame_stride, stride, w, h, fits, d_mask, (long long)w * h,
+                                      c->prm.thresh));
+    mark(c, 6);
+    return MDX_OK;
+}
+
+extern "C" void* mdx_dev_alloc(mdx_ctx* c, size_t bytes)
+{
+    if (!c) return nullptr;
+    hipSetDevice(c->device);
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+        set_err(c, MDX_ENOMEM, "hipMalloc(%zu) failed", bytes);
+        return nullptr;
+    }
+    return p;
+}
+
+extern "C" int mdx_dev_free(mdx_ctx* c, void* p)
+{
+    if (!c) return MDX_EINVAL;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    HIP_OR_RETURN(c, hipFree(p));
+    return MDX_OK;
+}
+
+extern "C" int mdx_memcpy_h2d(mdx_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c) return MDX_EINVAL;
+    HIP_OR_RETURN(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
+    return MDX_OK;
+}
+
+extern "C" int mdx_memcpy_d2h(mdx_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c) return MDX_EINVAL;
+    HIP_OR_RETURN(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
+    return MDX_OK;
+}

@@ -1,0 +1,73 @@
+// mdx_internal.h -- shared between the HIP kernels (mdx_kernels.hip) and the host API
+// (mdx_api.cpp).  Not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mdx {
+
+constexpr int kMaxLevels = 8;
+constexpr int kWin = 40;     // LK window side (reference optical_flow_calculator.cpp:41)
+constexpr int kPad = 40;     // border rows/cols every pyramid level carries (= win)
+constexpr int kXOff = 64;    // left margin of a level row: the core starts 64-B aligned
+
+// One pyramid level inside a per-pair slab.  Images are u8; derivatives are uint32 words
+// holding (Ix int16 | Iy int16 << 16), the little-endian image of OpenCV's interleaved
+// CV_16SC2 derivative Mat.  Both use the same pitch (elements) and origin.
+struct Level {
+    int w, h;              // core size
+    int pitch;             // elements per row (>= kXOff + w + kPad, multiple of 64)
+    int rows;              // kPad + h + kPad
+    long long img_off;     // byte offset of the level's padded buffer in the u8 slab
+    long long der_off;     // word offset of the level's padded buffer in the deriv slab
+    __host__ __device__ long long core() const { return (long long)kPad * pitch + kXOff; }
+};
+
+struct Geometry {
+    int nlev;                // attained maxLevel + 1
+    Level lv[kMaxLevels];
+    long long img_bytes;     // bytes of one pyramid slab (all levels)
+    long long der_words;     // words of one derivative slab (all levels)
+};
+
+// Per-pair result of the classify + fit stage.
+struct PairFit {
+    double H[9];      // getPerspectiveTransform output (or external H); zero when no fit
+    double Hinv[9];   // matrix warpPerspective actually samples with (inverse or all-zero)
+    int num_vectors;  // accepted vectors (reference return value)
+    int fit_status;   // 0 fitted, 1 no vectors, 2 fewer than 4 vectors
+    int pad_[2];
+};
+
+struct LkArgs {
+    const uint8_t* pyr1;     // prev pyramid slabs
+    const uint8_t* pyr2;     // next pyramid slabs
+    const uint32_t* der;     // prev derivative slabs
+    Geometry g;
+    int maxl;                // attained max level used by LK
+    int npts, ny, pixel_step;
+    int max_iters;
+    float min_eig;
+    double eps2;
+    float* next_pts;         // [batch][npts][2]
+    uint8_t* status;         // [batch][npts]
+};
+
+// Launchers (mdx_kernels.hip).  All enqueue on `s`.
+hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const uint8_t* in2, int w, int h,
+                           int stride, long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2,
+                           const Geometry& g);
+hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level);
+hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level);
+hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
+hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
+                               int ny, int pixel_step, double min_vector_size, double* vectors, PairFit* fits,
+                               int fit_mode, const double* H_external);
+hipError_t launch_set_fit_external(hipStream_t s, int batch, const double* H_external, PairFit* fits);
+hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,
+                            const uint8_t* g2, long long g2_stride, int g2_pitch, int w, int h,
+                            const PairFit* fits, uint8_t* mask, long long mask_stride, int thresh);
+hipError_t launch_export_fit(hipStream_t s, int batch, const PairFit* fits, double* H, int* num_vectors);
+
+}  // namespace mdx

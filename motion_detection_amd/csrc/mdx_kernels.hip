@@ -1,0 +1,815 @@
+// mdx_kernels.hip -- CDNA4 (gfx950) kernels of the flow + egomotion-warp + frame-diff path.
+//
+// Reference path: OpticalFlowCalculator::calculateOpticalFlow
+// (common/src/optical_flow_calculator.cpp:30-130).  Every kernel reproduces the arithmetic
+// of the OpenCV 2.4 routine the reference calls, bit for bit (integer stages exactly; float
+// and double stages in the same evaluation order, compiled with -ffp-contract=off so no
+// expression is fused into an FMA).  Stage map:
+//   A1      k_gray_pad       cvtColor(BGR2GRAY) on rgb8 + level-0 REFLECT_101 padding
+//   A3/A4   k_pyrdown        pyrDown + REFLECT_101 padding, both frames of every pair
+//   A3      k_scharr         calcSharrDeriv + CONSTANT-0 padding (prev frame)
+//   A5      k_lk             calcOpticalFlowPyrLK (LKTrackerInvoker, SSE2 summation order)
+//   A6/A7   k_classify_fit   Vec4d classification, first-4 getPerspectiveTransform, invert
+//   A8-A10  k_warp_diff      warpPerspective + absdiff + threshold, fused
+#include "mdx_internal.h"
+
+#include <float.h>
+#include <limits.h>
+
+namespace mdx {
+
+__device__ __forceinline__ int r101(int p, int len)
+{
+    // borderInterpolate(p, len, BORDER_REFLECT_101), any number of folds.
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        if (p < 0) p = -p;
+        else p = 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+// ------------------------------------------------------------------ A1: gray + pad
+// color.cpp RGB2Gray<uchar> with blueIdx 0 on rgb8 data (node.cpp:271 then :50):
+// gray = (R*1868 + G*9617 + B*4899 + 8192) >> 14.  mono8 passes through unchanged.
+// grid: x,y over the padded level-0 image, z = 2*pair + which frame.
+__global__ __launch_bounds__(256) void k_gray_pad(const uint8_t* __restrict__ in1, const uint8_t* __restrict__ in2,
+                                                  int w, int h, int stride, long long frame_stride, int fmt,
+                                                  uint8_t* __restrict__ pyr1, uint8_t* __restrict__ pyr2,
+                                                  long long img_bytes, Level L)
+{
+    const int which = blockIdx.z & 1, pair = blockIdx.z >> 1;
+    const int px = blockIdx.x * blockDim.x + threadIdx.x - kPad;
+    const int py = blockIdx.y * blockDim.y + threadIdx.y - kPad;
+    if (px >= w + kPad || py >= h + kPad) return;
+    const uint8_t* src = (which ? in2 : in1) + (long long)pair * frame_stride;
+    const int sx = r101(px, w), sy = r101(py, h);
+    const uint8_t* s = src + (long long)sy * stride;
+    int g;
+    if (fmt == 0) {
+        g = s[sx];
+    } else {
+        int r, gg, b;
+        if (fmt == 1) { r = s[3 * sx]; gg = s[3 * sx + 1]; b = s[3 * sx + 2]; }
+        else { b = s[3 * sx]; gg = s[3 * sx + 1]; r = s[3 * sx + 2]; }
+        g = (r * 1868 + gg * 9617 + b * 4899 + 8192) >> 14;
+    }
+    uint8_t* dst = (which ? pyr2 : pyr1) + (long long)pair * img_bytes + L.img_off + L.core();
+    dst[(long long)py * L.pitch + px] = (uint8_t)g;
+}
+
+// ------------------------------------------------------------------ A3/A4: pyrDown
+// pyramids.cpp pyrDown_<FixPtCast<uchar,8>>: dst(x,y) = (sum_ij k_i k_j src(r101(2y+i-2),
+// r101(2x+j-2)) + 128) >> 8, k = [1 4 6 4 1], on the source ROI's own size.  The source level
+// already carries its REFLECT_101 border (>= 2 px), so its taps are read straight from the
+// padded buffer; the destination border is the reflect-101 image of the destination core
+// (copyMakeBorder ... BORDER_REFLECT_101|BORDER_ISOLATED), computed in place.
+__global__ __launch_bounds__(256) void k_pyrdown(uint8_t* __restrict__ pyr1, uint8_t* __restrict__ pyr2,
+                                                 long long img_bytes, Level S, Level D)
+{
+    const int which = blockIdx.z & 1, pair = blockIdx.z >> 1;
+    const int px = blockIdx.x * blockDim.x + threadIdx.x - kPad;
+    const int py = blockIdx.y * blockDim.y + threadIdx.y - kPad;
+    if (px >= D.w + kPad || py >= D.h + kPad) return;
+    uint8_t* slab = (which ? pyr2 : pyr1) + (long long)pair * img_bytes;
+    const uint8_t* src = slab + S.img_off + S.core();
+    const int cx = r101(px, D.w), cy = r101(py, D.h);
+    const uint8_t* s0 = src + (long long)(2 * cy - 2) * S.pitch + (2 * cx - 2);
+    int acc = 0;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        const uint8_t* r = s0 + (long long)i * S.pitch;
+        int hrow = r[2] * 6 + (r[1] + r[3]) * 4 + r[0] + r[4];
+        const int ki = i == 2 ? 6 : (i == 1 || i == 3) ? 4 : 1;
+        acc += hrow * ki;
+    }
+    uint8_t* dst = slab + D.img_off + D.core();
+    dst[(long long)py * D.pitch + px] = (uint8_t)((acc + 128) >> 8);
+}
+
+// ------------------------------------------------------------------ A3: Scharr derivs
+// lkpyramid.cpp calcSharrDeriv.  Vertical t0 = 3(a+c)+10b, t1 = c-a; horizontal
+// Ix = t0[x+1]-t0[x-1], Iy = 3(t1[x-1]+t1[x+1])+10 t1[x].  OpenCV clamps the row/col
+// neighbours as reflect-101 (row -1 -> 1, col cols -> cols-2), which is exactly the padded
+// level's border, so the stencil reads the padded image directly.  Border = 0
+// (copyMakeBorder ... BORDER_CONSTANT).
+__global__ __launch_bounds__(256) void k_scharr(const uint8_t* __restrict__ pyr1, uint32_t* __restrict__ der,
+                                                long long img_bytes, long long der_words, Level L)
+{
+    const int pair = blockIdx.z;
+    const int px = blockIdx.x * blockDim.x + threadIdx.x - kPad;
+    const int py = blockIdx.y * blockDim.y + threadIdx.y - kPad;
+    if (px >= L.w + kPad || py >= L.h + kPad) return;
+    uint32_t* d = der + (long long)pair * der_words + L.der_off + L.core() + (long long)py * L.pitch + px;
+    if (px < 0 || py < 0 || px >= L.w || py >= L.h) { *d = 0u; return; }
+    const uint8_t* s = pyr1 + (long long)pair * img_bytes + L.img_off + L.core() + (long long)py * L.pitch + px;
+    const int p = L.pitch;
+    int t0m = (s[-p - 1] + s[p - 1]) * 3 + s[-1] * 10;
+    int t0p = (s[-p + 1] + s[p + 1]) * 3 + s[1] * 10;
+    int t1m = s[p - 1] - s[-p - 1];
+    int t1c = s[p] - s[-p];
+    int t1p = s[p + 1] - s[-p + 1];
+    int ix = t0p - t0m;
+    int iy = (t1m + t1p) * 3 + t1c * 10;
+    *d = (uint32_t)(uint16_t)(int16_t)ix | ((uint32_t)(uint16_t)(int16_t)iy << 16);
+}
+
+// ------------------------------------------------------------------ A5: LK tracker
+//
+// One 64-lane wave = one workgroup tracks PPW = 64/LPP grid points through every pyramid
+// level (LPP lanes per point).  Per level and point the 40x40 window is cut into 5 chunks of
+// R = 8 rows; each lane owns EC = 320/LPP window elements per chunk and keeps its
+// interpolated I*32, Ix, Iy for the whole level in registers (NE = 5*EC elements).
+//
+// Exact summation order.  OpenCV's SSE2 path accumulates every sum in four float lanes:
+// lane k takes window columns x = 4g+k in (row, g) order; A = ((P0+P1)+P2)+P3 and
+// b = (P0+P2)+(P1+P3).  A GPU reduction tree would round differently, so the kernel keeps
+// the reference's order: the lanes compute the per-element products (exact integer
+// products rounded once to float) in parallel and store them chain-ordered in LDS; then one
+// lane per chain (12 chains for A11/A12/A22, 8 for b1/b2) adds its 80 terms of the chunk in
+// order.  The result is bit-identical to the x86 reference, not merely within tolerance.
+template <int LPP>
+__global__ __launch_bounds__(64) void k_lk(LkArgs a)
+{
+    constexpr int WIN = 40, R = 8, NCH = WIN / R, EC = R * WIN / LPP, NE = NCH * EC, PPW = 64 / LPP;
+    constexpr int STRIDE = 88;                 // floats per chain (80 used; 4*odd => b128 conflict-free)
+    constexpr int PT_FLOATS = 12 * STRIDE + 16;
+    constexpr float HALFW = 19.5f;             // (winSize.width-1)*0.5f
+    constexpr float FLT_SCALE = 1.f / (1 << 20);
+    __shared__ float4 lds4[PPW * PT_FLOATS / 4];
+
+    const int lane = threadIdx.x;
+    const int p = lane / LPP, s = lane % LPP;
+    const int pt = blockIdx.x * PPW + p;
+    const int pair = blockIdx.y;
+    const bool valid = pt < a.npts;
+    float* ch = reinterpret_cast<float*>(lds4) + p * PT_FLOATS;
+    float* res = ch + 12 * STRIDE;
+
+    // element geometry (level independent)
+    int woff[EC], ex[EC], ey[EC];
+#pragma unroll
+    for (int i = 0; i < EC; i++) {
+        const int e = s + LPP * i;
+        ey[i] = e / WIN;
+        ex[i] = e % WIN;
+        woff[i] = (ex[i] & 3) * STRIDE + ey[i] * 10 + (ex[i] >> 2);
+    }
+
+    const int gx = valid ? pt / a.ny : 0, gy = valid ? pt % a.ny : 0;
+    const float px0 = (float)(gx * a.pixel_step), py0 = (float)(gy * a.pixel_step);
+    float npx = 0.f, npy = 0.f;   // nextPts[ptidx]
+    int status = 1;
+
+    uint32_t sd[NE];              // (Ix & 0xffff) | Iy << 16
+    uint32_t si[(NE + 1) / 2];    // I*32 values, two per word
+
+    const uint8_t* slab1 = a.pyr1 + (long long)pair * a.g.img_bytes;
+    const uint8_t* slab2 = a.pyr2 + (long long)pair * a.g.img_bytes;
+    const uint32_t* dslab = a.der + (long long)pair * a.g.der_words;
+
+    for (int level = a.maxl; level >= 0; --level) {
+        const Level L = a.g.lv[level];
+        const int pitch = L.pitch;
+        const uint8_t* Ib = slab1 + L.img_off + L.core();
+        const uint8_t* Jb = slab2 + L.img_off + L.core();
+        const uint32_t* Db = dslab + L.der_off + L.core();
+
+        const float scale = (float)(1. / (1 << level));
+        float ppx = px0 * scale, ppy = py0 * scale;
+        if (level == a.maxl) { npx = ppx; npy = ppy; }
+        else { npx = npx * 2.f; npy = npy * 2.f; }
+        ppx = ppx - HALFW;
+        ppy = ppy - HALFW;
+        const int ipx = (int)floorf(ppx), ipy = (int)floorf(ppy);
+        bool ok = valid && !(ipx < -WIN || ipx >= L.w || ipy < -WIN || ipy >= L.h);
+        if (valid && !ok && level == 0) status = 0;
+
+        int w00 = 0, w01 = 0, w10 = 0, w11 = 0;
+        if (ok) {
+            const float fa = ppx - (float)ipx, fb = ppy - (float)ipy;
+            w00 = __float2int_rn((1.f - fa) * (1.f - fb) * 16384.f);
+            w01 = __float2int_rn(fa * (1.f - fb) * 16384.f);
+            w10 = __float2int_rn((1.f - fa) * fb * 16384.f);
+            w11 = 16384 - w00 - w01 - w10;
+        }
+        int toff[EC];
+#pragma unroll
+        for (int i = 0; i < EC; i++) toff[i] = ey[i] * pitch + ex[i];
+        const int ibase = ipy * pitch + ipx;
+
+        // ---- window extraction + A sums (chains q*4+k, q: 0 A11, 1 A12, 2 A22)
+        float acc = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            if (ok) {
+#pragma unroll
+                for (int i = 0; i < EC; i++) {
+                    const int o = ibase + c * R * pitch + toff[i];
+                    const uint8_t* ip = Ib + o;
+                    const int ival = (ip[0] * w00 + ip[1] * w01 + ip[pitch] * w10 + ip[pitch + 1] * w11 + 256) >> 9;
+                    const uint32_t* dp = Db + o;
+                    const uint32_t d00 = dp[0], d01 = dp[1], d10 = dp[pitch], d11 = dp[pitch + 1];
+                    const int ixv = ((int)(int16_t)d00 * w00 + (int)(int16_t)d01 * w01 + (int)(int16_t)d10 * w10 +
+                                     (int)(int16_t)d11 * w11 + 8192) >> 14;
+                    const int iyv = (((int)d00 >> 16) * w00 + ((int)d01 >> 16) * w01 + ((int)d10 >> 16) * w10 +
+                                     ((int)d11 >> 16) * w11 + 8192) >> 14;
+                    const int k = c * EC + i;
+                    sd[k] = ((uint32_t)ixv & 0xffffu) | ((uint32_t)iyv << 16);
+                    if (k & 1) si[k >> 1] = (si[k >> 1] & 0xffffu) | ((uint32_t)ival << 16);
+                    else si[k >> 1] = (uint32_t)ival;
+                    float* wp = ch + woff[i];
+                    wp[0] = (float)(ixv * ixv);
+                    wp[4 * STRIDE] = (float)(ixv * iyv);
+                    wp[8 * STRIDE] = (float)(iyv * iyv);
+                }
+            }
+            __syncthreads();
+            if (ok && s < 12) {
+                const float4* cp = reinterpret_cast<const float4*>(ch + s * STRIDE);
+#pragma unroll
+                for (int t = 0; t < 20; t++) {
+                    const float4 v = cp[t];
+                    acc = acc + v.x; acc = acc + v.y; acc = acc + v.z; acc = acc + v.w;
+                }
+            }
+            __syncthreads();
+        }
+        if (ok && s < 12) res[s] = acc;
+        __syncthreads();
+
+        float A11 = 0.f, A12 = 0.f, A22 = 0.f, Dinv = 0.f;
+        if (ok) {
+            const float4 r0 = reinterpret_cast<const float4*>(res)[0];
+            const float4 r1 = reinterpret_cast<const float4*>(res)[1];
+            const float4 r2 = reinterpret_cast<const float4*>(res)[2];
+            A11 = ((r0.x + r0.y) + r0.z) + r0.w;
+            A12 = ((r1.x + r1.y) + r1.z) + r1.w;
+            A22 = ((r2.x + r2.y) + r2.z) + r2.w;
+            A11 = A11 * FLT_SCALE;
+            A12 = A12 * FLT_SCALE;
+            A22 = A22 * FLT_SCALE;
+            const float D = A11 * A22 - A12 * A12;
+            const float minEig = (A22 + A11 - __builtin_sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
+                                 (float)(2 * WIN * WIN);
+            if (minEig < a.min_eig || D < FLT_EPSILON) {
+                ok = false;
+                if (level == 0) status = 0;
+            } else {
+                Dinv = 1.f / D;
+            }
+        }
+        __syncthreads();   // res is rewritten by the iteration phase
+
+        // ---- Newton iterations
+        float nx = npx - HALFW, ny = npy - HALFW;
+        float pdx = 0.f, pdy = 0.f;
+        bool act = ok;
+        for (int j = 0; j < a.max_iters; j++) {
+            if (!__any(act)) break;
+            int jbase = 0, v00 = 0, v01 = 0, v10 = 0, v11 = 0;
+            if (act) {
+                const int inx = (int)floorf(nx), iny = (int)floorf(ny);
+                if (inx < -WIN || inx >= L.w || iny < -WIN || iny >= L.h) {
+                    act = false;
+                    if (level == 0) status = 0;
+                } else {
+                    const float fa = nx - (float)inx, fb = ny - (float)iny;
+                    v00 = __float2int_rn((1.f - fa) * (1.f - fb) * 16384.f);
+                    v01 = __float2int_rn(fa * (1.f - fb) * 16384.f);
+                    v10 = __float2int_rn((1.f - fa) * fb * 16384.f);
+                    v11 = 16384 - v00 - v01 - v10;
+                    jbase = iny * pitch + inx;
+                }
+            }
+            float bacc = 0.f;
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                if (act) {
+#pragma unroll
+                    for (int i = 0; i < EC; i++) {
+                        const uint8_t* jp = Jb + (jbase + c * R * pitch + toff[i]);
+                        const int jv = (jp[0] * v00 + jp[1] * v01 + jp[pitch] * v10 + jp[pitch + 1] * v11 + 256) >> 9;
+                        const int k = c * EC + i;
+                        const int iv = (k & 1) ? (int)(si[k >> 1] >> 16) : (int)(si[k >> 1] & 0xffffu);
+                        const int diff = jv - iv;
+                        const uint32_t dv = sd[k];
+                        float* wp = ch + woff[i];
+                        wp[0] = (float)(diff * (int)(int16_t)dv);
+                        wp[4 * STRIDE] = (float)(diff * ((int)dv >> 16));
+                    }
+                }
+                __syncthreads();
+                if (act && s < 8) {
+                    const float4* cp = reinterpret_cast<const float4*>(ch + s * STRIDE);
+#pragma unroll
+                    for (int t = 0; t < 20; t++) {
+                        const float4 v = cp[t];
+                        bacc = bacc + v.x; bacc = bacc + v.y; bacc = bacc + v.z; bacc = bacc + v.w;
+                    }
+                }
+                __syncthreads();
+            }
+            if (act && s < 8) res[s] = bacc;
+            __syncthreads();
+            if (act) {
+                const float4 q1 = reinterpret_cast<const float4*>(res)[0];
+                const float4 q2 = reinterpret_cast<const float4*>(res)[1];
+                float b1 = (q1.x + q1.z) + (q1.y + q1.w);
+                float b2 = (q2.x + q2.z) + (q2.y + q2.w);
+                b1 = b1 * FLT_SCALE;
+                b2 = b2 * FLT_SCALE;
+                const float dx = (A12 * b2 - A22 * b1) * Dinv;
+                const float dy = (A12 * b1 - A11 * b2) * Dinv;
+                nx = nx + dx;
+                ny = ny + dy;
+                npx = nx + HALFW;
+                npy = ny + HALFW;
+                if ((double)dx * dx + (double)dy * dy <= a.eps2) {
+                    act = false;
+                } else if (j > 0 && fabs((double)fabsf(dx + pdx)) < 0.01 && fabs((double)fabsf(dy + pdy)) < 0.01) {
+                    npx = npx - dx * 0.5f;
+                    npy = npy - dy * 0.5f;
+                    act = false;
+                }
+                pdx = dx;
+                pdy = dy;
+            }
+            __syncthreads();
+        }
+
+        if (level == 0 && valid && status) {
+            // err pass of LKTrackerInvoker: its final bounds check is observable (status).
+            const int fx = (int)floorf(npx - HALFW), fy = (int)floorf(npy - HALFW);
+            if (fx < -WIN || fx >= L.w || fy < -WIN || fy >= L.h) status = 0;
+        }
+    }
+
+    if (valid && s == 0) {
+        const long long o = (long long)pair * a.npts + pt;
+        a.next_pts[2 * o] = npx;
+        a.next_pts[2 * o + 1] = npy;
+        a.status[o] = (uint8_t)status;
+    }
+}
+
+// ------------------------------------------------------------------ A7: perspective fit
+// fdlibm __ieee754_hypot (what OpenCV's JacobiSVD reaches through ::hypot on glibc).
+__device__ double dev_hypot(double x, double y)
+{
+    auto hi = [](double d) { return (int)(__double_as_longlong(d) >> 32); };
+    auto lo = [](double d) { return (unsigned)(__double_as_longlong(d) & 0xffffffffll); };
+    auto set_hi = [](double d, int h) {
+        unsigned long long u = (unsigned long long)__double_as_longlong(d);
+        u = ((unsigned long long)(unsigned)h << 32) | (u & 0xffffffffull);
+        return __longlong_as_double((long long)u);
+    };
+    double a, b, t1, t2, y1, y2, w;
+    int j, k, ha, hb;
+    ha = hi(x) & 0x7fffffff;
+    hb = hi(y) & 0x7fffffff;
+    if (hb > ha) { a = y; b = x; j = ha; ha = hb; hb = j; }
+    else { a = x; b = y; }
+    a = set_hi(a, ha);
+    b = set_hi(b, hb);
+    if ((ha - hb) > 0x3c00000) return a + b;
+    k = 0;
+    if (ha > 0x5f300000) {
+        if (ha >= 0x7ff00000) {
+            w = a + b;
+            if (((ha & 0xfffff) | lo(a)) == 0) w = a;
+            if ((((unsigned)hb ^ 0x7ff00000u) | lo(b)) == 0) w = b;
+            return w;
+        }
+        ha -= 0x25800000; hb -= 0x25800000; k += 600;
+        a = set_hi(a, ha);
+        b = set_hi(b, hb);
+    }
+    if (hb < 0x20b00000) {
+        if (hb <= 0x000fffff) {
+            if ((hb | (int)lo(b)) == 0) return a;
+            t1 = set_hi(0.0, 0x7fd00000);
+            b *= t1;
+            a *= t1;
+            k -= 1022;
+        } else {
+            ha += 0x25800000; hb += 0x25800000; k -= 600;
+            a = set_hi(a, ha);
+            b = set_hi(b, hb);
+        }
+    }
+    w = a - b;
+    if (w > b) {
+        t1 = set_hi(0.0, ha);
+        t2 = a - t1;
+        w = __builtin_sqrt(t1 * t1 - (b * (-b) - t2 * (a + t1)));
+    } else {
+        a = a + a;
+        y1 = set_hi(0.0, hb);
+        y2 = b - y1;
+        t1 = set_hi(0.0, ha + 0x00100000);
+        t2 = a - t1;
+        w = __builtin_sqrt(t1 * y1 - (w * (-w) - (t1 * y2 + t2 * b)));
+    }
+    if (k != 0) {
+        t1 = set_hi(1.0, hi(1.0) + (k << 20));
+        return t1 * w;
+    }
+    return w;
+}
+
+// getPerspectiveTransform(src, dst) = solve(A, b, DECOMP_SVD) on the 8x8 DLT system:
+// lapack.cpp JacobiSVDImpl_<double> (one-sided Jacobi on A's columns, eps 10*DBL_EPSILON,
+// max(m,30) sweeps, descending sort) then SVBkSb (threshold 2*DBL_EPSILON*sum(w)).
+__device__ void dev_perspective_fit(const float* src, const float* dst, double* M)
+{
+    double At[64], Vt[64], W[8], bv[8], x[8];
+    for (int i = 0; i < 64; i++) At[i] = 0.0;
+    for (int i = 0; i < 4; i++) {
+        const float sx = src[2 * i], sy = src[2 * i + 1], dx = dst[2 * i], dy = dst[2 * i + 1];
+        // A[i][c] stored as At[c*8 + i]; rows i (x equations) and i+4 (y equations)
+        At[0 * 8 + i] = sx; At[1 * 8 + i] = sy; At[2 * 8 + i] = 1.0;
+        At[3 * 8 + i + 4] = sx; At[4 * 8 + i + 4] = sy; At[5 * 8 + i + 4] = 1.0;
+        At[6 * 8 + i] = (double)(-sx * dx);
+        At[7 * 8 + i] = (double)(-sy * dx);
+        At[6 * 8 + i + 4] = (double)(-sx * dy);
+        At[7 * 8 + i + 4] = (double)(-sy * dy);
+        bv[i] = dx;
+        bv[i + 4] = dy;
+    }
+    const int m = 8, n = 8;
+    const double eps = DBL_EPSILON * 10;
+    for (int i = 0; i < n; i++) {
+        double sd = 0;
+        for (int k = 0; k < m; k++) { const double t = At[i * m + k]; sd += t * t; }
+        W[i] = sd;
+        for (int k = 0; k < n; k++) Vt[i * n + k] = 0;
+        Vt[i * n + i] = 1;
+    }
+    for (int iter = 0; iter < 30; iter++) {
+        bool changed = false;
+        for (int i = 0; i < n - 1; i++)
+            for (int j = i + 1; j < n; j++) {
+                double* Ai = At + i * m;
+                double* Aj = At + j * m;
+                double aa = W[i], p = 0, bb = W[j];
+                for (int k = 0; k < m; k++) p += Ai[k] * Aj[k];
+                if (fabs(p) <= eps * __builtin_sqrt(aa * bb)) continue;
+                p *= 2;
+                const double beta = aa - bb, gamma = dev_hypot(p, beta);
+                double c, s;
+                if (beta < 0) {
+                    const double delta = (gamma - beta) * 0.5;
+                    s = __builtin_sqrt(delta / gamma);
+                    c = p / (gamma * s * 2);
+                } else {
+                    c = __builtin_sqrt((gamma + beta) / (gamma * 2));
+                    s = p / (gamma * c * 2);
+                }
+                aa = bb = 0;
+                for (int k = 0; k < m; k++) {
+                    const double t0 = c * Ai[k] + s * Aj[k];
+                    const double t1 = -s * Ai[k] + c * Aj[k];
+                    Ai[k] = t0; Aj[k] = t1;
+                    aa += t0 * t0; bb += t1 * t1;
+                }
+                W[i] = aa; W[j] = bb;
+                changed = true;
+                double* Vi = Vt + i * n;
+                double* Vj = Vt + j * n;
+                for (int k = 0; k < n; k++) {
+                    const double t0 = c * Vi[k] + s * Vj[k];
+                    const double t1 = -s * Vi[k] + c * Vj[k];
+                    Vi[k] = t0; Vj[k] = t1;
+                }
+            }
+        if (!changed) break;
+    }
+    for (int i = 0; i < n; i++) {
+        double sd = 0;
+        for (int k = 0; k < m; k++) { const double t = At[i * m + k]; sd += t * t; }
+        W[i] = __builtin_sqrt(sd);
+    }
+    for (int i = 0; i < n - 1; i++) {
+        int j = i;
+        for (int k = i + 1; k < n; k++) if (W[j] < W[k]) j = k;
+        if (i != j) {
+            double t = W[i]; W[i] = W[j]; W[j] = t;
+            for (int k = 0; k < m; k++) { t = At[i * m + k]; At[i * m + k] = At[j * m + k]; At[j * m + k] = t; }
+            for (int k = 0; k < n; k++) { t = Vt[i * n + k]; Vt[i * n + k] = Vt[j * n + k]; Vt[j * n + k] = t; }
+        }
+    }
+    // Left singular vectors: rows with W[i] <= DBL_MIN are skipped by the back-substitution
+    // threshold below, so only the normalisation of the others matters.
+    for (int i = 0; i < n; i++) {
+        if (W[i] <= DBL_MIN) continue;
+        const double s = 1 / W[i];
+        for (int k = 0; k < m; k++) At[i * m + k] *= s;
+    }
+    double threshold = 0;
+    for (int i = 0; i < n; i++) { x[i] = 0; threshold += W[i]; }
+    threshold *= DBL_EPSILON * 2;
+    for (int i = 0; i < n; i++) {
+        double wi = W[i];
+        if (fabs(wi) <= threshold) continue;
+        wi = 1 / wi;
+        double s = 0;
+        for (int j = 0; j < m; j++) s += At[i * m + j] * bv[j];
+        s *= wi;
+        for (int j = 0; j < n; j++) x[j] = x[j] + s * Vt[i * n + j];
+    }
+    for (int i = 0; i < 8; i++) M[i] = x[i];
+    M[8] = 1.;
+}
+
+// lapack.cpp invert(DECOMP_LU) for 3x3 CV_64F: cofactors times 1/det3; det == 0 -> zeros.
+__device__ void dev_invert3x3(const double* m, double* out)
+{
+    const double d0 = m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
+                      m[2] * (m[3] * m[7] - m[4] * m[6]);
+    if (d0 != 0.) {
+        const double d = 1. / d0;
+        out[0] = (m[4] * m[8] - m[5] * m[7]) * d;
+        out[1] = (m[2] * m[7] - m[1] * m[8]) * d;
+        out[2] = (m[1] * m[5] - m[2] * m[4]) * d;
+        out[3] = (m[5] * m[6] - m[3] * m[8]) * d;
+        out[4] = (m[0] * m[8] - m[2] * m[6]) * d;
+        out[5] = (m[2] * m[3] - m[0] * m[5]) * d;
+        out[6] = (m[3] * m[7] - m[4] * m[6]) * d;
+        out[7] = (m[1] * m[6] - m[0] * m[7]) * d;
+        out[8] = (m[0] * m[4] - m[1] * m[3]) * d;
+    } else {
+        for (int i = 0; i < 9; i++) out[i] = 0.0;
+    }
+}
+
+// A6 + A7: classify every grid point (optical_flow_calculator.cpp:78-117), count accepted
+// vectors, pick the first four accepted in x-major order, fit and invert.  One 256-thread
+// workgroup per pair; the first-4 search is a ballot scan that stops as soon as 4 are found
+// (only the count needs the full sweep).
+__global__ __launch_bounds__(256) void k_classify_fit(const float* __restrict__ next_pts, const uint8_t* __restrict__ status,
+                                                      int npts, int ny, int pixel_step, double mvs,
+                                                      double* __restrict__ vectors, PairFit* __restrict__ fits,
+                                                      int fit_mode, const double* __restrict__ H_ext)
+{
+    const int pair = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    __shared__ float s_src[8], s_dst[8];
+    __shared__ int s_wcnt[4];
+    __shared__ int s_total;
+    if (tid == 0) s_total = 0;
+    __syncthreads();
+    const float* np = next_pts + (long long)pair * npts * 2;
+    const uint8_t* st = status + (long long)pair * npts;
+    for (int base = 0; base < npts; base += 256) {
+        const int i = base + tid;
+        bool acc = false;
+        float sx = 0.f, sy = 0.f, ex = 0.f, ey = 0.f;
+        if (i < npts) {
+            sx = (float)((i / ny) * pixel_step);
+            sy = (float)((i % ny) * pixel_step);
+            ex = np[2 * i];
+            ey = np[2 * i + 1];
+            double v0, v1, v2, v3;
+            if (st[i]) {
+                const float xd = ex - sx, yd = ey - sy;
+                if (fabs((double)fabsf(xd)) > mvs || fabs((double)fabsf(yd)) > mvs) {
+                    acc = true;
+                    v0 = sx; v1 = sy; v2 = xd; v3 = yd;
+                } else {
+                    v0 = sx; v1 = sy; v2 = 0.0; v3 = 0.0;
+                }
+            } else {
+                v0 = -1.0; v1 = -1.0; v2 = 0.0; v3 = 0.0;
+            }
+            if (vectors) {
+                double* v = vectors + ((long long)pair * npts + i) * 4;
+                v[0] = v0; v[1] = v1; v[2] = v2; v[3] = v3;
+            }
+        }
+        const unsigned long long bal = __ballot(acc);
+        if (lane == 0) s_wcnt[wave] = __popcll(bal);
+        __syncthreads();
+        int before = s_total;
+        for (int w2 = 0; w2 < wave; w2++) before += s_wcnt[w2];
+        const int rank = before + __popcll(bal & ((1ull << lane) - 1ull));
+        if (acc && rank < 4) {
+            s_src[2 * rank] = sx; s_src[2 * rank + 1] = sy;
+            s_dst[2 * rank] = ex; s_dst[2 * rank + 1] = ey;
+        }
+        __syncthreads();
+        if (tid == 0) s_total += s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        PairFit& f = fits[pair];
+        const int total = s_total;
+        f.num_vectors = total;
+        if (fit_mode == 1) {
+            for (int k = 0; k < 9; k++) f.H[k] = H_ext[(long long)pair * 9 + k];
+            dev_invert3x3(f.H, f.Hinv);
+            f.fit_status = 0;
+        } else if (total >= 4) {
+            dev_perspective_fit(s_src, s_dst, f.H);
+            dev_invert3x3(f.H, f.Hinv);
+            f.fit_status = 0;
+        } else {
+            for (int k = 0; k < 9; k++) { f.H[k] = 0.0; f.Hinv[k] = 0.0; }
+            f.fit_status = total == 0 ? 1 : 2;
+        }
+    }
+}
+
+__global__ void k_set_fit_external(const double* __restrict__ H_ext, PairFit* __restrict__ fits, int batch)
+{
+    const int pair = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pair >= batch) return;
+    PairFit& f = fits[pair];
+    for (int k = 0; k < 9; k++) f.H[k] = H_ext[(long long)pair * 9 + k];
+    dev_invert3x3(f.H, f.Hinv);
+    f.num_vectors = 0;
+    f.fit_status = 0;
+}
+
+__global__ void k_export_fit(const PairFit* __restrict__ fits, int batch, double* H, int* num)
+{
+    const int pair = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pair >= batch) return;
+    if (H) for (int k = 0; k < 9; k++) H[(long long)pair * 9 + k] = fits[pair].H[k];
+    if (num) num[pair] = fits[pair].num_vectors;
+}
+
+// ------------------------------------------------------------------ A8-A10: warp + diff
+// warpPerspective(gray1, M) with M^-1 precomputed (fit.Hinv): imgwarp.cpp
+// warpPerspectiveInvoker, BLOCK_SZ 32 -> blocks of bw0 x bh0 (64 x 16 for W>=64, H>=16);
+// per pixel X = cvRound(clamp((X0 + M0*x1) * (W ? 32/W : 0))), W = W0 + M6*x1 with
+// X0 = M0*xb + M1*y + M2 at the block's left column xb; then remapBilinear with the 32x32
+// fixed-point table (weights (32-fx)(32-fy)*32 ..., +16384 >> 15) and BORDER_CONSTANT 0,
+// fused with absdiff and threshold: mask = |warp - gray2| > thresh ? 255 : 0.
+// A workgroup covers one 64 x 16 tile (the reference's block), 4 pixels per thread.
+__device__ __forceinline__ int clamp_int_from_double(double v)
+{
+    // std::max((double)INT_MIN, std::min((double)INT_MAX, v)) then cvRound
+    double r = (v < (double)INT_MAX) ? v : (double)INT_MAX;
+    r = ((double)INT_MIN < r) ? r : (double)INT_MIN;
+    return (int)__builtin_rint(r);
+}
+
+template <bool AFFINE>
+__device__ __forceinline__ void warp_coord(const double* M, double X0, double Y0, double W0, double Wc, int x1,
+                                           int& X, int& Y)
+{
+    double Wd;
+    if (AFFINE) {
+        Wd = Wc;
+    } else {
+        const double Wv = W0 + M[6] * x1;
+        Wd = Wv != 0.0 ? 32.0 / Wv : 0.0;
+    }
+    const double fX = (X0 + M[0] * x1) * Wd;
+    const double fY = (Y0 + M[3] * x1) * Wd;
+    X = clamp_int_from_double(fX);
+    Y = clamp_int_from_double(fY);
+}
+
+__global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
+                                                   const uint8_t* __restrict__ g2, long long g2_stride, int g2_pitch,
+                                                   int w, int h, int bw0, const PairFit* __restrict__ fits,
+                                                   uint8_t* __restrict__ mask, long long mask_stride, int thresh)
+{
+    const int pair = blockIdx.z;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int y = blockIdx.y * 16 + ty;
+    const int x0 = blockIdx.x * 64 + tx * 4;
+    if (y >= h || x0 >= w) return;
+    const PairFit& f = fits[pair];
+    uint8_t* mrow = mask + (long long)pair * mask_stride + (long long)y * w;
+    const int n = min(4, w - x0);
+    if (f.fit_status != 0) {
+        for (int k = 0; k < n; k++) mrow[x0 + k] = 0;
+        return;
+    }
+    double M[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) M[k] = f.Hinv[k];
+    const bool affine = (M[6] == 0.0) && (M[7] == 0.0);
+    const double Wc = M[8] != 0.0 ? 32.0 / M[8] : 0.0;
+    const uint8_t* src = g1 + (long long)pair * g1_stride;
+    const uint8_t* r2 = g2 + (long long)pair * g2_stride + (long long)y * g2_pitch;
+    uint8_t out[4] = {0, 0, 0, 0};
+    int xb_prev = -1;
+    double X0 = 0, Y0 = 0, W0 = 0;
+    for (int k = 0; k < n; k++) {
+        const int x = x0 + k;
+        const int xb = (x / bw0) * bw0, x1 = x - xb;
+        if (xb != xb_prev) {
+            X0 = M[0] * xb + M[1] * y + M[2];
+            Y0 = M[3] * xb + M[4] * y + M[5];
+            W0 = M[6] * xb + M[7] * y + M[8];
+            xb_prev = xb;
+        }
+        int X, Y;
+        if (affine) warp_coord<true>(M, X0, Y0, W0, Wc, x1, X, Y);
+        else warp_coord<false>(M, X0, Y0, W0, Wc, x1, X, Y);
+        const int sx = min(max(X >> 5, -32768), 32767), sy = min(max(Y >> 5, -32768), 32767);
+        const int fx = X & 31, fy = Y & 31;
+        // (0,0) cell of BilinearTab_i is {32767,0,0,1}; for 8-bit data it yields the same
+        // value as {32768,0,0,0}, which is what the plain formula below computes.
+        const int wt0 = (32 - fx) * (32 - fy) * 32, wt1 = fx * (32 - fy) * 32;
+        const int wt2 = (32 - fx) * fy * 32, wt3 = fx * fy * 32;
+        const bool ix0 = (unsigned)sx < (unsigned)w, ix1 = (unsigned)(sx + 1) < (unsigned)w;
+        const bool iy0 = (unsigned)sy < (unsigned)h, iy1 = (unsigned)(sy + 1) < (unsigned)h;
+        const int cx0 = min(max(sx, 0), w - 1), cx1 = min(max(sx + 1, 0), w - 1);
+        const int cy0 = min(max(sy, 0), h - 1), cy1 = min(max(sy + 1, 0), h - 1);
+        const uint8_t* ra = src + (long long)cy0 * g1_pitch;
+        const uint8_t* rb = src + (long long)cy1 * g1_pitch;
+        const int v0 = (ix0 && iy0) ? ra[cx0] : 0;
+        const int v1 = (ix1 && iy0) ? ra[cx1] : 0;
+        const int v2 = (ix0 && iy1) ? rb[cx0] : 0;
+        const int v3 = (ix1 && iy1) ? rb[cx1] : 0;
+        int v = (v0 * wt0 + v1 * wt1 + v2 * wt2 + v3 * wt3 + (1 << 14)) >> 15;
+        v = min(max(v, 0), 255);
+        const int d = abs(v - (int)r2[x]);
+        out[k] = d > thresh ? 255 : 0;
+    }
+    if (n == 4 && ((((uintptr_t)(mrow + x0)) & 3) == 0)) {
+        *reinterpret_cast<uchar4*>(mrow + x0) = make_uchar4(out[0], out[1], out[2], out[3]);
+    } else {
+        for (int k = 0; k < n; k++) mrow[x0 + k] = out[k];
+    }
+}
+
+// ------------------------------------------------------------------ launchers
+static inline dim3 padded_grid(int w, int h, int z, dim3 blk)
+{
+    return dim3((w + 2 * kPad + blk.x - 1) / blk.x, (h + 2 * kPad + blk.y - 1) / blk.y, z);
+}
+
+hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const uint8_t* in2, int w, int h, int stride,
+                           long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g)
+{
+    const dim3 blk(64, 4);
+    hipLaunchKernelGGL(k_gray_pad, padded_grid(w, h, 2 * batch, blk), blk, 0, s, in1, in2, w, h, stride, frame_stride,
+                       fmt, pyr1, pyr2, g.img_bytes, g.lv[0]);
+    return hipGetLastError();
+}
+
+hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level)
+{
+    const dim3 blk(64, 4);
+    const Level& D = g.lv[level];
+    hipLaunchKernelGGL(k_pyrdown, padded_grid(D.w, D.h, 2 * batch, blk), blk, 0, s, pyr1, pyr2, g.img_bytes,
+                       g.lv[level - 1], D);
+    return hipGetLastError();
+}
+
+hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level)
+{
+    const dim3 blk(64, 4);
+    const Level& L = g.lv[level];
+    hipLaunchKernelGGL(k_scharr, padded_grid(L.w, L.h, batch, blk), blk, 0, s, pyr1, der, g.img_bytes, g.der_words, L);
+    return hipGetLastError();
+}
+
+hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a)
+{
+    constexpr int LPP = 32, PPW = 64 / LPP;
+    const dim3 grid((a.npts + PPW - 1) / PPW, batch);
+    hipLaunchKernelGGL(k_lk<LPP>, grid, dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
+                               int ny, int pixel_step, double mvs, double* vectors, PairFit* fits, int fit_mode,
+                               const double* H_external)
+{
+    hipLaunchKernelGGL(k_classify_fit, dim3(batch), dim3(256), 0, s, next_pts, status, npts, ny, pixel_step, mvs,
+                       vectors, fits, fit_mode, H_external);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_fit_external(hipStream_t s, int batch, const double* H_external, PairFit* fits)
+{
+    hipLaunchKernelGGL(k_set_fit_external, dim3((batch + 63) / 64), dim3(64), 0, s, H_external, fits, batch);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_fit(hipStream_t s, int batch, const PairFit* fits, double* H, int* num)
+{
+    hipLaunchKernelGGL(k_export_fit, dim3((batch + 63) / 64), dim3(64), 0, s, fits, batch, H, num);
+    return hipGetLastError();
+}
+
+hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,
+                            const uint8_t* g2, long long g2_stride, int g2_pitch, int w, int h, const PairFit* fits,
+                            uint8_t* mask, long long mask_stride, int thresh)
+{
+    const int bh0 = h < 16 ? h : 16;
+    const int bw0 = (1024 / bh0) < w ? (1024 / bh0) : w;
+    const dim3 grid((w + 63) / 64, (h + 15) / 16, batch);
+    hipLaunchKernelGGL(k_warp_diff, grid, dim3(256), 0, s, g1, g1_stride, g1_pitch, g2, g2_stride, g2_pitch, w, h, bw0,
+                       fits, mask, mask_stride, thresh);
+    return hipGetLastError();
+}
+
+}  // namespace mdx

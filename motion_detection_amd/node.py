@@ -1,0 +1,106 @@
+"""ROS-free core of MotionDetectionNode for the hot path (the drop-in boundary's caller).
+
+Reproduces the ingest semantics of MotionDetectionNode::imageCallback
+(ros/src/motion_detection_node.cpp:235-287) and the runOpticalFlow caller (:76-92), without
+ROS: frames arrive as ``Image`` records shaped like sensor_msgs/Image (height, width,
+encoding, step, data).  Parameters mirror the node's ROS params (:29-44, :237-245):
+
+* skip_frames (default 1) and num_motions (default 2) are re-read on every frame;
+  trajectory_size = 2*num_motions + 1, or 2 when egomotion is false (:241-245).
+* a frame is dropped unless global_frame_count % skip_frames == 0 (:247).  Like the
+  reference, the counter only advances on dropped frames, so skip_frames > 1 keeps every
+  frame once the counter is a multiple of skip_frames; the mirror keeps that quirk.
+* raw frames go into a ring of trajectory_size (:248-261); once full, the last two
+  frames are converted to rgb8 (cv_bridge toCvCopy, :271) and handed to the calculator.
+
+Publishing is a callback: ``on_result(result)`` receives the FlowResult (vectors + mask),
+standing in for publishImage on ~optical_flow_image (:83-85).
+"""
+from __future__ import annotations
+
+from collections import deque
+from dataclasses import dataclass
+from typing import Callable
+
+import numpy as np
+
+from . import _lib
+from .optical_flow_calculator import OpticalFlowCalculator
+
+ENCODINGS = {"mono8": (1, _lib.FMT_GRAY8), "rgb8": (3, _lib.FMT_RGB8), "bgr8": (3, _lib.FMT_BGR8)}
+
+
+@dataclass
+class Image:
+    """Minimal sensor_msgs/Image."""
+    height: int
+    width: int
+    encoding: str
+    step: int
+    data: bytes | np.ndarray
+
+    @staticmethod
+    def from_array(a: np.ndarray, encoding: str | None = None) -> "Image":
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        enc = encoding or ("mono8" if a.ndim == 2 else "rgb8")
+        return Image(a.shape[0], a.shape[1], enc, a.strides[0], a.tobytes())
+
+
+def to_rgb8(msg: Image) -> np.ndarray:
+    """cv_bridge::toCvCopy(msg, "rgb8"): mono8 is replicated, bgr8 is reordered."""
+    if msg.encoding not in ENCODINGS:
+        raise ValueError(f"unsupported encoding {msg.encoding!r}")
+    cn, _ = ENCODINGS[msg.encoding]
+    buf = np.frombuffer(bytes(msg.data) if not isinstance(msg.data, np.ndarray) else msg.data.tobytes(), np.uint8)
+    rows = buf[: msg.step * msg.height].reshape(msg.height, msg.step)[:, : msg.width * cn]
+    if cn == 1:
+        return np.repeat(rows[:, :, None], 3, axis=2)
+    px = rows.reshape(msg.height, msg.width, 3)
+    return px[:, :, ::-1].copy() if msg.encoding == "bgr8" else px.copy()
+
+
+class MotionDetectionNode:
+    def __init__(self, params: dict | None = None, on_result: Callable | None = None, device: int = 0):
+        self.params = {"pixel_step": 10, "min_vector_size": 1.0, "skip_frames": 1, "num_motions": 2,
+                       "egomotion": False, "use_all_frames": True}
+        if params:
+            self.params.update(params)
+        self.on_result = on_result
+        self.raw_images: deque = deque()
+        self.global_frame_count = 0
+        self.image_received = False
+        self.frames_processed = 0
+        self.ofc = OpticalFlowCalculator(device=device)
+
+    @property
+    def trajectory_size(self) -> int:
+        # node.cpp:241-245
+        return 2 if not self.params["egomotion"] else 2 * int(self.params["num_motions"]) + 1
+
+    def image_callback(self, msg: Image):
+        skip = int(self.params.get("skip_frames", 1))
+        if self.global_frame_count % skip != 0:          # :247
+            self.global_frame_count += 1
+            return None
+        ts = self.trajectory_size
+        if len(self.raw_images) < ts:                     # :248-261
+            self.raw_images.append(msg)
+            if len(self.raw_images) == ts:
+                self.image_received = True
+        else:
+            self.raw_images.append(msg)
+            self.raw_images.popleft()
+            self.image_received = True
+        if not (self.params.get("use_all_frames", True) and self.image_received):
+            return None
+        frames = [to_rgb8(m) for m in list(self.raw_images)[-2:]]   # :266-287
+        return self.run_optical_flow(frames[0], frames[1])
+
+    def run_optical_flow(self, image1: np.ndarray, image2: np.ndarray):
+        """runOpticalFlow (node.cpp:76-92)."""
+        res = self.ofc.compute(image1, image2, int(self.params["pixel_step"]), float(self.params["min_vector_size"]),
+                               fmt=_lib.FMT_RGB8)
+        self.frames_processed += 1
+        if self.on_result is not None:
+            self.on_result(res)
+        return res

@@ -1,0 +1,104 @@
+/*
+ * mdx_oracle.h -- CPU restatement of the reference hot path (TEST INFRASTRUCTURE ONLY).
+ *
+ * This header and oracle/mdx_oracle.c are the parity ORACLE for the MI355X path in
+ * motion_detection_amd/.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it; the product library never links it.
+ *
+ * What it restates: OpticalFlowCalculator::calculateOpticalFlow
+ * (reference common/src/optical_flow_calculator.cpp:30-130) and the OpenCV calls it makes.
+ * OpenCV is a third-party dependency that is NOT vendored in /root/reference and NOT
+ * installed here.  The semantics restated are those of OpenCV 2.4.8 (ROS Indigo's
+ * opencv2 package; the reference uses 2.4-only APIs) on an x86-64 SSE2 build:
+ *   cvtColor(CV_BGR2GRAY)            color.cpp    RGB2Gray<uchar>            (call site :50-51)
+ *   buildOpticalFlowPyramid          lkpyramid.cpp + pyramids.cpp pyrDown_   (:67)
+ *   calcOpticalFlowPyrLK             lkpyramid.cpp LKTrackerInvoker, SSE2 order (:71)
+ *   getPerspectiveTransform          imgwarp.cpp + lapack.cpp JacobiSVD/SVBkSb (:120)
+ *   warpPerspective                  imgwarp.cpp warpPerspectiveInvoker + remapBilinear (:124)
+ *   absdiff / threshold(190,255,BINARY)                                       (:125,:127)
+ *
+ * Parity status: UNPINNED against a real OpenCV 2.4 binary -- the reference ships no
+ * tests, fixtures or golden vectors and OpenCV cannot be built or
+ * imported here.  The oracle is pinned instead by known-answer tests and by an
+ * independent numpy restatement (tests/golden/make_golden.py); see DESIGN.md §3.
+ */
+#ifndef MDX_ORACLE_H_
+#define MDX_ORACLE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORA_MAX_LEVELS 16
+
+enum { ORA_FMT_GRAY8 = 0, ORA_FMT_RGB8 = 1, ORA_FMT_BGR8 = 2 };
+
+typedef struct {
+    int win;             /* window side, reference 40 (optical_flow_calculator.cpp:41) */
+    int max_level;       /* reference MAX_LEVEL 5 (:40) */
+    int max_iters;       /* TermCriteria count 10 (:44) */
+    double eps;          /* TermCriteria eps 0.03 (:44) */
+    float min_eig;       /* minEigThreshold 1e-3 (:71) */
+    int thresh;          /* threshold 190 (:127) */
+    int pixel_step;      /* ROS param pixel_step (motion_detection_node.cpp:29) */
+    double min_vector_size; /* ROS param min_vector_size, default 1.0 (node.cpp:44) */
+} ora_params;
+
+void ora_default_params(ora_params* p);
+
+/* One pyramid: per level a padded u8 image and (optionally) padded interleaved Ix,Iy int16. */
+typedef struct {
+    int nlevels;                 /* attained maxLevel + 1 */
+    int pad;                     /* = win */
+    int w[ORA_MAX_LEVELS], h[ORA_MAX_LEVELS];
+    uint8_t* img[ORA_MAX_LEVELS];    /* (h+2pad) x (w+2pad), pitch w+2pad, REFLECT_101 border */
+    int16_t* deriv[ORA_MAX_LEVELS];  /* (h+2pad) x (w+2pad) x 2, CONSTANT-0 border; NULL if none */
+} ora_pyramid;
+
+int  ora_reflect101(int p, int len);
+void ora_to_gray(const uint8_t* src, int w, int h, int stride, int fmt, uint8_t* dst);
+void ora_pyrdown(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh, int dstride);
+void ora_scharr(const uint8_t* src, int w, int h, int sstride, int16_t* dst, int dstride);
+int  ora_build_pyramid(const uint8_t* gray, int w, int h, int win, int max_level, int with_deriv, ora_pyramid* out);
+void ora_free_pyramid(ora_pyramid* p);
+
+/* calcOpticalFlowPyrLK over a prev pyramid (with derivs) and next pyramid; nthreads>=1. */
+void ora_lk(const ora_pyramid* prev, const ora_pyramid* next, int max_level,
+            const float* prev_pts, float* next_pts, uint8_t* status, int npts,
+            const ora_params* prm, int nthreads);
+
+void ora_get_perspective_transform(const float src[8], const float dst[8], double M[9]);
+int  ora_invert3x3(const double M[9], double Minv[9]);
+void ora_warp_perspective(const uint8_t* src, int w, int h, int sstride, const double M[9],
+                          uint8_t* dst, int dstride, int nthreads);
+void ora_absdiff_threshold(const uint8_t* a, const uint8_t* b, int n, int thresh, uint8_t* mask);
+
+/* Grid of the reference (optical_flow_calculator.cpp:56-64): x-major order. */
+int  ora_grid_count(int w, int h, int pixel_step);
+void ora_grid_points(int w, int h, int pixel_step, float* pts);
+
+/*
+ * Whole hot path.  Outputs (any may be NULL):
+ *   next_pts  2*npts floats  (LK output points, x-major grid order)
+ *   status    npts bytes
+ *   vectors   4*npts doubles (x, y, dx, dy) / (x, y, 0, 0) / (-1, -1, 0, 0)  (:78-117)
+ *   mask      w*h bytes      (only written when num_vectors >= 4, else zero-filled)
+ *   H         9 doubles      (getPerspectiveTransform result; zero when no fit)
+ *   Hinv      9 doubles      (matrix actually used by the warp: inverse or all-zero)
+ * Returns num_vectors.  *fit_status: 0 = fitted, 1 = num_vectors==0 (no mask, :118),
+ * 2 = 1..3 vectors (reference UB at :120; defined here as "no fit, zero mask").
+ */
+int ora_calculate_optical_flow(const uint8_t* img1, const uint8_t* img2, int w, int h, int stride,
+                               int fmt, const ora_params* prm, int nthreads,
+                               float* next_pts, uint8_t* status, double* vectors,
+                               uint8_t* mask, double* H, double* Hinv, int* fit_status);
+
+/* Synthetic-frame generator spec is in the product (motion_detection_amd/csrc/synth.cpp);
+ * the oracle does not need one. */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,177 @@
+"""ctypes binding of the C oracle (oracle/mdx_oracle.c).  TEST INFRASTRUCTURE ONLY.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg; the product
+package (motion_detection_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libmdx_oracle.so")
+_lib = None
+
+FMT_GRAY8, FMT_RGB8, FMT_BGR8 = 0, 1, 2
+
+
+class OraParams(C.Structure):
+    _fields_ = [("win", C.c_int), ("max_level", C.c_int), ("max_iters", C.c_int),
+                ("eps", C.c_double), ("min_eig", C.c_float), ("thresh", C.c_int),
+                ("pixel_step", C.c_int), ("min_vector_size", C.c_double)]
+
+
+MAXL = 16
+
+
+class OraPyramid(C.Structure):
+    _fields_ = [("nlevels", C.c_int), ("pad", C.c_int), ("w", C.c_int * MAXL), ("h", C.c_int * MAXL),
+                ("img", C.POINTER(C.c_uint8) * MAXL), ("deriv", C.POINTER(C.c_int16) * MAXL)]
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its Makefile (gcc is present on the GPU box too)."""
+    src = os.path.join(_HERE, "mdx_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(_LIB_PATH)
+        u8p, f32p, f64p, i16p = (C.POINTER(C.c_uint8), C.POINTER(C.c_float),
+                                 C.POINTER(C.c_double), C.POINTER(C.c_int16))
+        L.ora_default_params.argtypes = [C.POINTER(OraParams)]
+        L.ora_to_gray.argtypes = [u8p, C.c_int, C.c_int, C.c_int, C.c_int, u8p]
+        L.ora_pyrdown.argtypes = [u8p, C.c_int, C.c_int, C.c_int, u8p, C.c_int, C.c_int, C.c_int]
+        L.ora_scharr.argtypes = [u8p, C.c_int, C.c_int, C.c_int, i16p, C.c_int]
+        L.ora_build_pyramid.argtypes = [u8p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(OraPyramid)]
+        L.ora_build_pyramid.restype = C.c_int
+        L.ora_free_pyramid.argtypes = [C.POINTER(OraPyramid)]
+        L.ora_lk.argtypes = [C.POINTER(OraPyramid), C.POINTER(OraPyramid), C.c_int, f32p, f32p, u8p,
+                             C.c_int, C.POINTER(OraParams), C.c_int]
+        L.ora_get_perspective_transform.argtypes = [f32p, f32p, f64p]
+        L.ora_invert3x3.argtypes = [f64p, f64p]
+        L.ora_invert3x3.restype = C.c_int
+        L.ora_warp_perspective.argtypes = [u8p, C.c_int, C.c_int, C.c_int, f64p, u8p, C.c_int, C.c_int]
+        L.ora_absdiff_threshold.argtypes = [u8p, u8p, C.c_int, C.c_int, u8p]
+        L.ora_grid_count.argtypes = [C.c_int, C.c_int, C.c_int]
+        L.ora_grid_count.restype = C.c_int
+        L.ora_calculate_optical_flow.argtypes = [u8p, u8p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                 C.POINTER(OraParams), C.c_int, f32p, u8p, f64p, u8p,
+                                                 f64p, f64p, C.POINTER(C.c_int)]
+        L.ora_calculate_optical_flow.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def params(**kw) -> OraParams:
+    p = OraParams()
+    lib().ora_default_params(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def to_gray(img: np.ndarray, fmt: int | None = None) -> np.ndarray:
+    img = np.ascontiguousarray(img)
+    h, w = img.shape[:2]
+    if fmt is None:
+        fmt = FMT_GRAY8 if img.ndim == 2 else FMT_RGB8
+    out = np.empty((h, w), np.uint8)
+    lib().ora_to_gray(_p(img, C.c_uint8), w, h, img.strides[0], fmt, _p(out, C.c_uint8))
+    return out
+
+
+def pyrdown(src: np.ndarray) -> np.ndarray:
+    src = np.ascontiguousarray(src)
+    h, w = src.shape
+    dst = np.empty(((h + 1) // 2, (w + 1) // 2), np.uint8)
+    lib().ora_pyrdown(_p(src, C.c_uint8), w, h, w, _p(dst, C.c_uint8), dst.shape[1], dst.shape[0], dst.shape[1])
+    return dst
+
+
+def scharr(src: np.ndarray) -> np.ndarray:
+    src = np.ascontiguousarray(src)
+    h, w = src.shape
+    dst = np.empty((h, w, 2), np.int16)
+    lib().ora_scharr(_p(src, C.c_uint8), w, h, w, _p(dst, C.c_int16), 2 * w)
+    return dst
+
+
+def build_pyramid(gray: np.ndarray, win: int = 40, max_level: int = 5, with_deriv: bool = True):
+    """Returns (max_level_attained, [padded u8 levels], [padded int16 (h,w,2) derivs or None])."""
+    gray = np.ascontiguousarray(gray)
+    h, w = gray.shape
+    P = OraPyramid()
+    ml = lib().ora_build_pyramid(_p(gray, C.c_uint8), w, h, win, max_level, int(with_deriv), C.byref(P))
+    imgs, ders = [], []
+    for l in range(P.nlevels):
+        lw, lh = P.w[l] + 2 * win, P.h[l] + 2 * win
+        imgs.append(np.ctypeslib.as_array(P.img[l], shape=(lh, lw)).copy())
+        ders.append(np.ctypeslib.as_array(P.deriv[l], shape=(lh, lw, 2)).copy() if with_deriv else None)
+    lib().ora_free_pyramid(C.byref(P))
+    return ml, imgs, ders
+
+
+def warp_perspective(src: np.ndarray, Minv: np.ndarray, nthreads: int = 1) -> np.ndarray:
+    src = np.ascontiguousarray(src)
+    h, w = src.shape
+    M = np.ascontiguousarray(Minv, dtype=np.float64).ravel()
+    dst = np.empty_like(src)
+    lib().ora_warp_perspective(_p(src, C.c_uint8), w, h, w, _p(M, C.c_double), _p(dst, C.c_uint8), w, nthreads)
+    return dst
+
+
+def get_perspective_transform(src4: np.ndarray, dst4: np.ndarray) -> np.ndarray:
+    s = np.ascontiguousarray(src4, dtype=np.float32).ravel()
+    d = np.ascontiguousarray(dst4, dtype=np.float32).ravel()
+    M = np.zeros(9)
+    lib().ora_get_perspective_transform(_p(s, C.c_float), _p(d, C.c_float), _p(M, C.c_double))
+    return M.reshape(3, 3)
+
+
+def invert3x3(M: np.ndarray) -> np.ndarray:
+    m = np.ascontiguousarray(M, dtype=np.float64).ravel()
+    out = np.zeros(9)
+    lib().ora_invert3x3(_p(m, C.c_double), _p(out, C.c_double))
+    return out.reshape(3, 3)
+
+
+def grid_count(w: int, h: int, ps: int) -> int:
+    return lib().ora_grid_count(w, h, ps)
+
+
+def calculate_optical_flow(img1: np.ndarray, img2: np.ndarray, fmt: int | None = None, nthreads: int = 1,
+                           want_mask: bool = True, **kw):
+    """Whole reference path.  Returns dict like motion_detection_amd's result."""
+    img1 = np.ascontiguousarray(img1)
+    img2 = np.ascontiguousarray(img2)
+    h, w = img1.shape[:2]
+    if fmt is None:
+        fmt = FMT_GRAY8 if img1.ndim == 2 else FMT_RGB8
+    prm = params(**kw)
+    n = grid_count(w, h, prm.pixel_step)
+    nextp = np.zeros((n, 2), np.float32)
+    status = np.zeros(n, np.uint8)
+    vec = np.zeros((n, 4), np.float64)
+    mask = np.zeros((h, w), np.uint8) if want_mask else None
+    H = np.zeros(9)
+    Hinv = np.zeros(9)
+    fs = C.c_int(0)
+    num = lib().ora_calculate_optical_flow(
+        _p(img1, C.c_uint8), _p(img2, C.c_uint8), w, h, img1.strides[0], fmt, C.byref(prm), nthreads,
+        _p(nextp, C.c_float), _p(status, C.c_uint8), _p(vec, C.c_double),
+        _p(mask, C.c_uint8) if mask is not None else None, _p(H, C.c_double), _p(Hinv, C.c_double), C.byref(fs))
+    return dict(num_vectors=num, next_pts=nextp, status=status, vectors=vec, mask=mask,
+                H=H.reshape(3, 3), Hinv=Hinv.reshape(3, 3), fit_status=fs.value)

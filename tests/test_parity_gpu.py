@@ -1,0 +1,188 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle, bit for bit.
+
+Bar: LK output points are compared as float32 bit patterns and must be
+identical (the kernel reproduces the reference's SSE2 summation order), status / Vec4d
+vectors / num_vectors / H / mask must be identical too.  The north-star tolerance
+(1e-4 relative on flow) is therefore met with margin 0.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(res, ref, label=""):
+    assert res.num_vectors == ref["num_vectors"], label
+    np.testing.assert_array_equal(res.status, ref["status"], err_msg=label)
+    bad = np.nonzero(res.next_pts.view(np.uint32) != ref["next_pts"].view(np.uint32))[0]
+    assert bad.size == 0, f"{label}: {bad.size} LK points differ, first {bad[:5]}: " \
+                          f"{res.next_pts[bad[:3]]} vs {ref['next_pts'][bad[:3]]}"
+    np.testing.assert_array_equal(res.vectors, ref["vectors"], err_msg=label)
+    np.testing.assert_array_equal(res.H.view(np.uint64), ref["H"].view(np.uint64), err_msg=label)
+    if res.mask is not None:
+        nbad = int((res.mask != ref["mask"]).sum())
+        assert nbad == 0, f"{label}: {nbad} mask pixels differ"
+
+
+CASES = [
+    # (w, h, pixel_step, channels, seed)
+    (160, 120, 10, 1, 1),
+    (640, 480, 10, 1, 20141105),
+    (640, 480, 3, 1, 7),
+    (333, 241, 7, 1, 11),
+    (320, 240, 10, 3, 5),
+    (1920, 1080, 10, 1, 20141106),
+]
+
+
+@pytest.mark.parametrize("w,h,ps,ch,seed", CASES)
+def test_full_path_bit_exact(mdx, ctx, oracle, w, h, ps, ch, seed):
+    a, b, _ = mdx.synth_pair(seed, w, h, ch)
+    ctx.set_params(pixel_step=ps, min_vector_size=1.0, fit_mode=mdx.FIT_FIRST4)
+    res = ctx.flow_warp_diff(a, b)
+    ref = oracle.calculate_optical_flow(a, b, nthreads=8, pixel_step=ps, min_vector_size=1.0)
+    _compare(res, ref, f"{w}x{h} ps{ps} ch{ch}")
+
+
+def test_bgr_input(mdx, ctx, oracle):
+    a, b, _ = mdx.synth_pair(3, 320, 240, 3)
+    ctx.set_params(pixel_step=10, min_vector_size=0.4, fit_mode=mdx.FIT_FIRST4)
+    res = ctx.flow_warp_diff(a, b, fmt=mdx.FMT_BGR8)
+    ref = oracle.calculate_optical_flow(a, b, fmt=oracle.FMT_BGR8, pixel_step=10, min_vector_size=0.4)
+    _compare(res, ref, "bgr8")
+
+
+def test_translation_known_answer(mdx, ctx, oracle):
+    """Integer translation of a textured scene: flow == shift to LK precision, bit-exact vs oracle."""
+    big, _, _ = mdx.synth_pair(99, 400, 300, 1)
+    a = np.ascontiguousarray(big[20:260, 20:340])
+    b = np.ascontiguousarray(big[17:257, 15:335])   # scene moves by (+5, +3)
+    ctx.set_params(pixel_step=10, min_vector_size=1.0, fit_mode=mdx.FIT_FIRST4)
+    res = ctx.flow_warp_diff(a, b)
+    ref = oracle.calculate_optical_flow(a, b, pixel_step=10)
+    _compare(res, ref, "translation")
+    d = res.next_pts - mdx.grid_points(320, 240, 10)
+    inner = (res.status == 1)
+    med = np.median(d[inner], axis=0)
+    assert abs(med[0] - 5) < 0.05 and abs(med[1] - 3) < 0.05
+
+
+def test_flat_frames_no_vectors(mdx, ctx, oracle):
+    """Constant frames: every minEig test fails -> status 0, no vectors, no mask (:118)."""
+    a = np.full((120, 160), 77, np.uint8)
+    ctx.set_params(pixel_step=10, fit_mode=mdx.FIT_FIRST4)
+    res = ctx.flow_warp_diff(a, a.copy())
+    ref = oracle.calculate_optical_flow(a, a.copy(), pixel_step=10)
+    assert res.num_vectors == 0 and res.code == mdx.MDX_EDEGENERATE
+    assert res.status.sum() == 0
+    _compare(res, ref, "flat")
+    assert res.mask.max() == 0
+
+
+def test_identical_frames(mdx, ctx, oracle):
+    a, _, _ = mdx.synth_pair(4, 200, 150, 1)
+    res = ctx.flow_warp_diff(a, a.copy())
+    ref = oracle.calculate_optical_flow(a, a.copy(), pixel_step=ctx.params.pixel_step)
+    _compare(res, ref, "identical")
+
+
+@pytest.mark.parametrize("w,h", [(48, 48), (41, 90), (63, 45), (81, 81)])
+def test_small_frames(mdx, ctx, oracle, w, h):
+    """Single-level pyramids, widths below the 64-px warp block, reflect-101 multi-folds."""
+    a, b, _ = mdx.synth_pair(w * 1000 + h, w, h, 1)
+    ctx.set_params(pixel_step=5, min_vector_size=1.0, fit_mode=mdx.FIT_FIRST4)
+    res = ctx.flow_warp_diff(a, b)
+    ref = oracle.calculate_optical_flow(a, b, pixel_step=5)
+    _compare(res, ref, f"{w}x{h}")
+
+
+def _projective(w, h):
+    return np.array([[1.002, 0.013, -2.5], [-0.011, 0.995, 1.75], [2.1e-5, -1.3e-5, 1.0]])
+
+
+@pytest.mark.parametrize("kind", ["true_affine", "projective", "singular"])
+def test_external_h_warp(mdx, ctx, oracle, kind):
+    w, h = 640, 480
+    a, b, Ht = mdx.synth_pair(21, w, h, 1)
+    H = {"true_affine": Ht, "projective": _projective(w, h), "singular": np.zeros((3, 3))}[kind]
+    ctx.set_params(pixel_step=10, fit_mode=mdx.FIT_EXTERNAL)
+    try:
+        res = ctx.flow_warp_diff(a, b, H_external=H)
+    finally:
+        ctx.set_params(fit_mode=mdx.FIT_FIRST4)
+    Hinv = oracle.invert3x3(H)
+    warped = oracle.warp_perspective(a, Hinv)
+    d = np.abs(warped.astype(np.int16) - b.astype(np.int16))
+    ref_mask = np.where(d > 190, 255, 0).astype(np.uint8)
+    assert int((res.mask != ref_mask).sum()) == 0
+    np.testing.assert_array_equal(res.H, H)
+
+
+def test_warp_diff_dev_batch(mdx, ctx, oracle):
+    """The standalone fused warp+diff entry over a batch with per-pair H (roofline kernel)."""
+    w, h, B = 500, 300, 3
+    frames1, frames2, Hs = [], [], []
+    for i in range(B):
+        a, b, Ht = mdx.synth_pair(100 + i, w, h, 1)
+        frames1.append(a); frames2.append(b)
+        Hs.append(Ht if i != 1 else _projective(w, h))
+    g1 = np.stack(frames1); g2 = np.stack(frames2); Hb = np.stack(Hs).astype(np.float64)
+    d1, d2, dH, dM = (ctx.dev_alloc(x) for x in (g1.nbytes, g2.nbytes, Hb.nbytes, B * w * h))
+    try:
+        ctx.h2d(d1, g1); ctx.h2d(d2, g2); ctx.h2d(dH, Hb)
+        ctx.warp_diff_dev(B, d1, d2, w, h, w, w * h, dH, dM)
+        ctx.sync()
+        out = np.empty((B, h, w), np.uint8)
+        ctx.d2h(out, dM)
+    finally:
+        for p in (d1, d2, dH, dM):
+            ctx.dev_free(p)
+    for i in range(B):
+        warped = oracle.warp_perspective(g1[i], oracle.invert3x3(Hb[i]))
+        ref = np.where(np.abs(warped.astype(np.int16) - g2[i].astype(np.int16)) > 190, 255, 0).astype(np.uint8)
+        assert int((out[i] != ref).sum()) == 0, f"pair {i}"
+
+
+def test_batch_dev_matches_host_path(mdx, oracle):
+    """The zero-copy batched entry gives the same per-pair results as the oracle."""
+    w, h, B = 320, 240, 4
+    pairs = [mdx.synth_pair(300 + i, w, h, 1) for i in range(B)]
+    g1 = np.stack([p[0] for p in pairs]); g2 = np.stack([p[1] for p in pairs])
+    n = mdx.grid_count(w, h, 10)
+    with mdx.Context(0, w, h, B) as c:
+        c.set_params(pixel_step=10)
+        bufs = {k: c.dev_alloc(s) for k, s in dict(i1=g1.nbytes, i2=g2.nbytes, np=B * n * 8, st=B * n,
+                                                    vec=B * n * 32, mask=B * w * h, H=B * 72, num=B * 4).items()}
+        c.h2d(bufs["i1"], g1); c.h2d(bufs["i2"], g2)
+        c.flow_warp_diff_batch_dev(B, bufs["i1"], bufs["i2"], w, h, w, w * h, mdx.FMT_GRAY8, bufs["np"], bufs["st"],
+                                   bufs["vec"], bufs["mask"], bufs["H"], 0, bufs["num"])
+        c.sync()
+        out = dict(np=np.empty((B, n, 2), np.float32), st=np.empty((B, n), np.uint8), vec=np.empty((B, n, 4)),
+                   mask=np.empty((B, h, w), np.uint8), H=np.empty((B, 3, 3)), num=np.empty(B, np.int32))
+        for k, arr in out.items():
+            c.d2h(arr, bufs[k])
+        for p in bufs.values():
+            c.dev_free(p)
+    for i in range(B):
+        ref = oracle.calculate_optical_flow(g1[i], g2[i], pixel_step=10)
+        assert out["num"][i] == ref["num_vectors"]
+        np.testing.assert_array_equal(out["st"][i], ref["status"])
+        np.testing.assert_array_equal(out["np"][i].view(np.uint32), ref["next_pts"].view(np.uint32))
+        np.testing.assert_array_equal(out["vec"][i], ref["vectors"])
+        np.testing.assert_array_equal(out["mask"][i], ref["mask"])
+        np.testing.assert_array_equal(out["H"][i], ref["H"])
+
+
+def test_reference_interface(mdx, oracle):
+    """OpticalFlowCalculator.calculateOpticalFlow fills the vector Mat and comp like the reference."""
+    a, b, _ = mdx.synth_pair(8, 320, 240, 3)
+    ofc = mdx.OpticalFlowCalculator(max_w=320, max_h=240)
+    vec = np.zeros((240, 320, 4))
+    comp = np.zeros((240, 320), np.uint8)
+    num = ofc.calculateOpticalFlow(a, b, vec, 10, comp, 1.0)
+    ref = oracle.calculate_optical_flow(a, b, pixel_step=10, min_vector_size=1.0)
+    assert num == ref["num_vectors"]
+    pts = mdx.grid_points(320, 240, 10).astype(int)
+    np.testing.assert_array_equal(vec[pts[:, 1], pts[:, 0]], ref["vectors"])
+    np.testing.assert_array_equal(comp, ref["mask"])
+    ofc.close()
