@@ -81,6 +81,8 @@ int mdx_get_params(const mdx_ctx* ctx, mdx_params* p);
 void* mdx_stream(mdx_ctx* ctx);
 int mdx_device(const mdx_ctx* ctx);
 int mdx_sync(mdx_ctx* ctx);
+/* hipDeviceSynchronize on the context's device (all streams). */
+int mdx_device_sync(mdx_ctx* ctx);
 
 /*
  * Synchronous host-buffer entry: the direct replacement of calculateOpticalFlow.
@@ -136,10 +138,13 @@ int mdx_dev_free(mdx_ctx* ctx, void* p);
 int mdx_memcpy_h2d(mdx_ctx* ctx, void* dst, const void* src, size_t bytes);
 int mdx_memcpy_d2h(mdx_ctx* ctx, void* dst, const void* src, size_t bytes);
 
-/* Timing of the most recent batched call, per stage, from HIP events on the ctx stream
- * (milliseconds). stage: 0 gray+pad, 1 pyramids, 2 Scharr, 3 LK, 4 classify+fit,
- * 5 warp+diff, 6 total.  Enabled by mdx_enable_timing(ctx, 1). */
+/* Per-stage device time from HIP events recorded on the ctx stream around each stage.
+ * mdx_enable_timing(ctx, 1) (re)starts recording; every later pipeline call records one
+ * event set (up to 256 calls).  mdx_stage_ms returns the SUM over the recorded calls, in
+ * milliseconds, of stage: 0 gray+pad, 1 pyramids, 2 Scharr, 3 LK, 4 classify+fit,
+ * 5 warp+diff, 6 whole call; mdx_timing_calls returns how many calls were recorded. */
 int mdx_enable_timing(mdx_ctx* ctx, int on);
+int mdx_timing_calls(const mdx_ctx* ctx);
 int mdx_stage_ms(mdx_ctx* ctx, int stage, float* ms);
 
 /*

@@ -27,8 +27,9 @@ FIT_FIRST4, FIT_EXTERNAL = 0, 1
 EXPORTED = [
     "mdx_default_params", "mdx_grid_count", "mdx_create", "mdx_create_error", "mdx_destroy",
     "mdx_last_error", "mdx_set_params", "mdx_get_params", "mdx_stream", "mdx_device", "mdx_sync",
+    "mdx_device_sync",
     "mdx_flow_warp_diff", "mdx_flow_warp_diff_batch_dev", "mdx_warp_diff_dev", "mdx_dev_alloc",
-    "mdx_dev_free", "mdx_memcpy_h2d", "mdx_memcpy_d2h", "mdx_enable_timing", "mdx_stage_ms",
+    "mdx_dev_free", "mdx_memcpy_h2d", "mdx_memcpy_d2h", "mdx_enable_timing", "mdx_timing_calls", "mdx_stage_ms",
     "mdx_synth_pair",
 ]
 
@@ -84,6 +85,8 @@ def lib() -> C.CDLL:
     L.mdx_device.restype = C.c_int
     L.mdx_sync.argtypes = [vp]
     L.mdx_sync.restype = C.c_int
+    L.mdx_device_sync.argtypes = [vp]
+    L.mdx_device_sync.restype = C.c_int
     L.mdx_flow_warp_diff.argtypes = [vp, u8p, u8p, C.c_int, C.c_int, C.c_int, C.c_int, f32p, u8p, f64p, u8p,
                                      f64p, f64p, C.POINTER(C.c_int)]
     L.mdx_flow_warp_diff.restype = C.c_int
@@ -102,6 +105,8 @@ def lib() -> C.CDLL:
     L.mdx_memcpy_d2h.restype = C.c_int
     L.mdx_enable_timing.argtypes = [vp, C.c_int]
     L.mdx_enable_timing.restype = C.c_int
+    L.mdx_timing_calls.argtypes = [vp]
+    L.mdx_timing_calls.restype = C.c_int
     L.mdx_stage_ms.argtypes = [vp, C.c_int, C.POINTER(C.c_float)]
     L.mdx_stage_ms.restype = C.c_int
     L.mdx_synth_pair.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, u8p, u8p, f64p, C.c_int]

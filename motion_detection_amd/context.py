@@ -129,6 +129,9 @@ class Context:
     def sync(self):
         self._check(lib().mdx_sync(self._h))
 
+    def device_sync(self):
+        self._check(lib().mdx_device_sync(self._h))
+
     @property
     def stream(self) -> int:
         return lib().mdx_stream(self._h) or 0
@@ -137,8 +140,9 @@ class Context:
         self._check(lib().mdx_enable_timing(self._h, int(on)))
 
     def stage_ms(self) -> dict:
+        """Per-stage device ms summed over the calls since enable_timing(); 'calls' = count."""
         names = ["gray_pad", "pyrdown", "scharr", "lk", "classify_fit", "warp_diff", "total"]
-        out = {}
+        out = {"calls": lib().mdx_timing_calls(self._h)}
         for i, nm in enumerate(names):
             ms = C.c_float(0)
             self._check(lib().mdx_stage_ms(self._h, i, C.byref(ms)))

@@ -30,7 +30,10 @@ struct mdx_ctx {
     DevBuf in1, in2, np, st, vec, mask, H, Hext, num;   // host-path staging
     DevBuf bnp, bst;                         // LK outputs the batched caller did not ask for
     bool timing = false;
-    hipEvent_t ev[8] = {};
+    static constexpr int kSlots = 256;     // timed calls kept between mdx_enable_timing and readout
+    hipEvent_t* ev = nullptr;              // kSlots x 7 events
+    int ncalls = 0;                        // calls recorded since enable
+    int cur = -1;                          // slot of the call in flight
     std::string err;
 };
 
@@ -114,8 +117,8 @@ static int ensure(mdx_ctx* c, DevBuf& b, size_t need)
     if (need == 0) need = 1;
     if (b.p && b.cap >= need) return MDX_OK;
     if (b.p) {
-        hipStreamSynchronize(c->stream);
-        hipFree(b.p);
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(b.p);
         b.p = nullptr;
         b.cap = 0;
     }
@@ -163,7 +166,6 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
         delete c;
         return nullptr;
     }
-    for (auto& e : c->ev) hipEventCreate(&e);
     Geometry g = make_geometry(max_w, max_h, prm.max_level);
     if (ensure_workspace(c, g, max_batch) != MDX_OK) {
         g_create_err = c->err;
@@ -176,15 +178,17 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
 extern "C" int mdx_destroy(mdx_ctx* c)
 {
     if (!c) return MDX_EINVAL;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->pyr1, &c->pyr2, &c->der, &c->fits, &c->in1, &c->in2, &c->np, &c->st,
                       &c->vec, &c->mask, &c->H, &c->Hext, &c->num, &c->bnp, &c->bst};
     for (DevBuf* b : bufs)
-        if (b->p) hipFree(b->p);
-    for (auto& e : c->ev)
-        if (e) hipEventDestroy(e);
-    if (c->stream) hipStreamDestroy(c->stream);
+        if (b->p) (void)hipFree(b->p);
+    if (c->ev) {
+        for (int i = 0; i < mdx_ctx::kSlots * 7; i++) (void)hipEventDestroy(c->ev[i]);
+        delete[] c->ev;
+    }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return MDX_OK;
 }
@@ -216,26 +220,57 @@ extern "C" int mdx_sync(mdx_ctx* c)
     return MDX_OK;
 }
 
-extern "C" int mdx_enable_timing(mdx_ctx* c, int on)
+extern "C" int mdx_device_sync(mdx_ctx* c)
 {
     if (!c) return MDX_EINVAL;
-    c->timing = on != 0;
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    HIP_OR_RETURN(c, hipDeviceSynchronize());
     return MDX_OK;
 }
 
+extern "C" int mdx_enable_timing(mdx_ctx* c, int on)
+{
+    if (!c) return MDX_EINVAL;
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    if (on && !c->ev) {
+        c->ev = new hipEvent_t[mdx_ctx::kSlots * 7];
+        for (int i = 0; i < mdx_ctx::kSlots * 7; i++) HIP_OR_RETURN(c, hipEventCreate(&c->ev[i]));
+    }
+    c->timing = on != 0;
+    c->ncalls = 0;
+    c->cur = -1;
+    return MDX_OK;
+}
+
+extern "C" int mdx_timing_calls(const mdx_ctx* c) { return c ? c->ncalls : 0; }
+
+// Sum over the recorded calls of the time between the stage's bracketing events.
 extern "C" int mdx_stage_ms(mdx_ctx* c, int stage, float* ms)
 {
     if (!c || !ms || stage < 0 || stage > 6) return MDX_EINVAL;
-    if (!c->timing) return set_err(c, MDX_EINVAL, "timing not enabled");
-    HIP_OR_RETURN(c, hipEventSynchronize(c->ev[6]));
-    if (stage == 6) HIP_OR_RETURN(c, hipEventElapsedTime(ms, c->ev[0], c->ev[6]));
-    else HIP_OR_RETURN(c, hipEventElapsedTime(ms, c->ev[stage], c->ev[stage + 1]));
+    if (!c->timing || !c->ev) return set_err(c, MDX_EINVAL, "timing not enabled");
+    if (c->ncalls > mdx_ctx::kSlots) return set_err(c, MDX_EINVAL, "more than %d timed calls", mdx_ctx::kSlots);
+    float total = 0.f;
+    for (int k = 0; k < c->ncalls; k++) {
+        hipEvent_t* e = c->ev + k * 7;
+        HIP_OR_RETURN(c, hipEventSynchronize(e[6]));
+        float t = 0.f;
+        if (stage == 6) HIP_OR_RETURN(c, hipEventElapsedTime(&t, e[0], e[6]));
+        else HIP_OR_RETURN(c, hipEventElapsedTime(&t, e[stage], e[stage + 1]));
+        total += t;
+    }
+    *ms = total;
     return MDX_OK;
 }
 
 static inline void mark(mdx_ctx* c, int i)
 {
-    if (c->timing) hipEventRecord(c->ev[i], c->stream);
+    if (!c->timing || !c->ev) return;
+    if (i == 0) {
+        c->cur = c->ncalls < mdx_ctx::kSlots ? c->ncalls : -1;
+        c->ncalls++;
+    }
+    if (c->cur >= 0) (void)hipEventRecord(c->ev[c->cur * 7 + i], c->stream);
 }
 
 // The pipeline on device buffers.  d_np/d_st must be valid (LK writes them).
@@ -385,8 +420,7 @@ extern "C" int mdx_warp_diff_dev(mdx_ctx* c, int batch, const uint8_t* d_gray1, 
     if (rc != MDX_OK) return rc;
     hipStream_t s = c->stream;
     PairFit* fits = c->fits.as<PairFit>();
-    mark(c, 0);
-    for (int i = 1; i < 5; i++) mark(c, i);
+    for (int i = 0; i < 5; i++) mark(c, i);
     HIP_OR_RETURN(c, launch_set_fit_external(s, batch, d_H, fits));
     mark(c, 5);
     HIP_OR_RETURN(c, launch_warp_diff(s, batch, d_gray1, (long long)frame_stride, stride, d_gray2,
@@ -399,7 +433,7 @@ extern "C" int mdx_warp_diff_dev(mdx_ctx* c, int batch, const uint8_t* d_gray1, 
 extern "C" void* mdx_dev_alloc(mdx_ctx* c, size_t bytes)
 {
     if (!c) return nullptr;
-    hipSetDevice(c->device);
+    (void)hipSetDevice(c->device);
     void* p = nullptr;
     if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
         set_err(c, MDX_ENOMEM, "hipMalloc(%zu) failed", bytes);
@@ -411,8 +445,8 @@ extern "C" void* mdx_dev_alloc(mdx_ctx* c, size_t bytes)
 extern "C" int mdx_dev_free(mdx_ctx* c, void* p)
 {
     if (!c) return MDX_EINVAL;
-    hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
     HIP_OR_RETURN(c, hipFree(p));
     return MDX_OK;
 }
