@@ -147,6 +147,10 @@ int mdx_enable_timing(mdx_ctx* ctx, int on);
 int mdx_timing_calls(const mdx_ctx* ctx);
 int mdx_stage_ms(mdx_ctx* ctx, int stage, float* ms);
 
+/* Test hook: copy an internal buffer of the last call to the host (0: per-(pair, level,
+ * point) float4 LK gradient sums; 1: per-level LK trace when MDX_LK_DEBUG=1 at create). */
+int mdx_debug_copy(mdx_ctx* ctx, int which, void* dst, size_t bytes);
+
 /*
  * Synthetic frame-pair generator used by the benchmark and tests (host, deterministic,
  * byte-identical on every x86-64 host).  Spec in DESIGN.md §5: blurred value noise +

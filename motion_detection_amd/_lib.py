@@ -30,7 +30,7 @@ EXPORTED = [
     "mdx_device_sync",
     "mdx_flow_warp_diff", "mdx_flow_warp_diff_batch_dev", "mdx_warp_diff_dev", "mdx_dev_alloc",
     "mdx_dev_free", "mdx_memcpy_h2d", "mdx_memcpy_d2h", "mdx_enable_timing", "mdx_timing_calls", "mdx_stage_ms",
-    "mdx_synth_pair",
+    "mdx_synth_pair", "mdx_debug_copy",
 ]
 
 
@@ -109,6 +109,8 @@ def lib() -> C.CDLL:
     L.mdx_timing_calls.restype = C.c_int
     L.mdx_stage_ms.argtypes = [vp, C.c_int, C.POINTER(C.c_float)]
     L.mdx_stage_ms.restype = C.c_int
+    L.mdx_debug_copy.argtypes = [vp, C.c_int, vp, C.c_size_t]
+    L.mdx_debug_copy.restype = C.c_int
     L.mdx_synth_pair.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, u8p, u8p, f64p, C.c_int]
     L.mdx_synth_pair.restype = C.c_int
     _lib = L

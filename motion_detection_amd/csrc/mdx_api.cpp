@@ -12,6 +12,8 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
+#include <cstdlib>
 
 using namespace mdx;
 
@@ -29,6 +31,12 @@ struct mdx_ctx {
     DevBuf pyr1, pyr2, der, fits;            // pyramid / derivative / fit workspace
     DevBuf in1, in2, np, st, vec, mask, H, Hext, num;   // host-path staging
     DevBuf bnp, bst;                         // LK outputs the batched caller did not ask for
+    DevBuf cls, Abuf, ctab;                  // LK v2: class planes, A sums, residue tables
+    DevBuf dbg;                              // LK v2 per-level trace (MDX_LK_DEBUG=1)
+    bool lk_debug = false;
+    int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
+    int plan_w = -1, plan_h = -1, plan_ps = -1, plan_ml = -1;
+    ClassPlan plan{};
     bool timing = false;
     static constexpr int kSlots = 256;     // timed calls kept between mdx_enable_timing and readout
     hipEvent_t* ev = nullptr;              // kSlots x 7 events
@@ -96,7 +104,7 @@ static Geometry make_geometry(int w, int h, int max_level)
         Level& L = g.lv[lvl];
         L.w = sw;
         L.h = sh;
-        L.pitch = (kXOff + sw + kPad + 63) / 64 * 64;
+        L.pitch = (kXOff + sw + kPad + 16 + 63) / 64 * 64;   // +16: slack for 16-B row loads
         L.rows = kPad + sh + kPad;
         L.img_off = img;
         L.der_off = der;
@@ -140,6 +148,59 @@ static int ensure_workspace(mdx_ctx* c, const Geometry& g, int batch)
     return MDX_OK;
 }
 
+// Residue classes of the grid at each level (see mdx_lk.hip) and the class-plane layout.
+// Tables are rebuilt and uploaded only when the frame size / pixel_step / level count change.
+static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps, int batch)
+{
+    int rc;
+    if (c->plan_w != w || c->plan_h != h || c->plan_ps != ps || c->plan_ml != g.nlev) {
+        const int nx = (w + ps - 1) / ps, ny = (h + ps - 1) / ps;
+        static_assert(kMaxLevels <= 8, "residue tables sized for 2^7 residues");
+        std::vector<int16_t> tab(2 * kMaxLevels * 2 * 128, (int16_t)-1);
+        int16_t* cmap = tab.data();
+        int16_t* rlist = tab.data() + kMaxLevels * 2 * 128;
+        ClassPlan P{};
+        long long off = 0;
+        for (int l = 0; l < g.nlev; l++) {
+            const int m = (1 << l) - 1;
+            int n[2] = {0, 0};
+            for (int axis = 0; axis < 2; axis++) {
+                const int cnt = axis == 0 ? nx : ny;
+                for (int i = 0; i < cnt; i++) {
+                    const int r = (i * ps) & m;
+                    int16_t& slot = cmap[(l * 2 + axis) * 128 + r];
+                    if (slot < 0) {
+                        slot = (int16_t)n[axis];
+                        rlist[(l * 2 + axis) * 128 + n[axis]] = (int16_t)r;
+                        n[axis]++;
+                    }
+                    if (n[axis] == m + 1) break;
+                }
+            }
+            ClassLevel& C = P.lv[l];
+            C.nrx = n[0];
+            C.nry = n[1];
+            C.UH = g.lv[l].h + 79;
+            C.PW = (g.lv[l].w + 82) / 4 + 4;
+            C.class_elems = 4LL * C.UH * C.PW;
+            C.off = off;
+            off += (long long)C.nrx * C.nry * C.class_elems;
+        }
+        P.elems_per_pair = (off + 31) / 32 * 32;
+        if ((rc = ensure(c, c->ctab, tab.size() * sizeof(int16_t))) != MDX_OK) return rc;
+        HIP_OR_RETURN(c, hipMemcpy(c->ctab.p, tab.data(), tab.size() * sizeof(int16_t), hipMemcpyHostToDevice));
+        c->plan = P;
+        c->plan_w = w;
+        c->plan_h = h;
+        c->plan_ps = ps;
+        c->plan_ml = g.nlev;
+    }
+    const int npts = mdx_grid_count(w, h, ps);
+    if ((rc = ensure(c, c->cls, (size_t)c->plan.elems_per_pair * 8 * batch)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->Abuf, (size_t)npts * g.nlev * 16 * batch)) != MDX_OK) return rc;
+    return MDX_OK;
+}
+
 extern "C" const char* mdx_create_error(void) { return g_create_err.c_str(); }
 
 extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, const mdx_params* p)
@@ -161,6 +222,8 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     c->max_w = max_w;
     c->max_h = max_h;
     c->max_batch = max_batch;
+    if (const char* e = std::getenv("MDX_LK_IMPL")) c->lk_impl = std::atoi(e) == 1 ? 1 : 2;
+    if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         g_create_err = "hipStreamCreate failed";
         delete c;
@@ -181,7 +244,8 @@ extern "C" int mdx_destroy(mdx_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->pyr1, &c->pyr2, &c->der, &c->fits, &c->in1, &c->in2, &c->np, &c->st,
-                      &c->vec, &c->mask, &c->H, &c->Hext, &c->num, &c->bnp, &c->bst};
+                      &c->vec, &c->mask, &c->H, &c->Hext, &c->num, &c->bnp, &c->bst,
+                      &c->cls, &c->Abuf, &c->ctab, &c->dbg};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (c->ev) {
@@ -320,7 +384,22 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         a.eps2 = e * e;
         a.next_pts = d_np;
         a.status = d_st;
-        HIP_OR_RETURN(c, launch_lk(s, batch, a));
+        if (c->lk_impl == 1) {
+            HIP_OR_RETURN(c, launch_lk(s, batch, a));
+        } else {
+            if ((rc = ensure_class_plan(c, g, w, h, P.pixel_step, batch)) != MDX_OK) return rc;
+            a.plan = c->plan;
+            a.cmap = c->ctab.as<int16_t>();
+            a.rlist = c->ctab.as<int16_t>() + kMaxLevels * 2 * 128;
+            if (c->lk_debug) {
+                if ((rc = ensure(c, c->dbg, ((size_t)npts * g.nlev * batch + kMaxLevels * 64) * 16)) != MDX_OK)
+                    return rc;
+                a.dbg = c->dbg.as<float4>();
+                const char* e = std::getenv("MDX_LK_DEBUG_PT");
+                a.dbg_pt = e ? std::atoi(e) : -1;
+            }
+            HIP_OR_RETURN(c, launch_lk_v2(s, batch, a, c->cls.as<uint2>(), c->Abuf.as<float4>()));
+        }
     }
     mark(c, 4);
     HIP_OR_RETURN(c, launch_classify_fit(s, batch, d_np, d_st, npts, ny, P.pixel_step, P.min_vector_size, d_vec, fits,
@@ -427,6 +506,18 @@ extern "C" int mdx_warp_diff_dev(mdx_ctx* c, int batch, const uint8_t* d_gray1, 
                                       (long long)frame_stride, stride, w, h, fits, d_mask, (long long)w * h,
                                       c->prm.thresh));
     mark(c, 6);
+    return MDX_OK;
+}
+
+// Test hook: copy an internal LK v2 buffer to the host (0 = A sums, 1 = per-level trace).
+extern "C" int mdx_debug_copy(mdx_ctx* c, int which, void* dst, size_t bytes)
+{
+    if (!c || !dst) return MDX_EINVAL;
+    DevBuf& b = which == 0 ? c->Abuf : which == 1 ? c->dbg : which == 2 ? c->pyr1 : which == 3 ? c->pyr2
+              : which == 4 ? c->der : c->cls;
+    if (!b.p) return set_err(c, MDX_EINVAL, "debug buffer %d unavailable", which);
+    HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
+    HIP_OR_RETURN(c, hipMemcpy(dst, b.p, bytes < b.cap ? bytes : b.cap, hipMemcpyDeviceToHost));
     return MDX_OK;
 }
 

@@ -40,6 +40,28 @@ struct PairFit {
     int pad_[2];
 };
 
+// Residue-class planes of LK v2 (mdx_lk.hip): per level, one plane set per class of
+// (P_x mod 2^L, P_y mod 2^L) present in the grid.  Each class holds 4 planes (column mod 4)
+// of UH x PW elements; an element is uint2(Ix | Iy << 16, I*32).
+struct ClassLevel {
+    int nrx, nry;            // residue classes per axis
+    int UH, PW;              // plane rows (h + 79), plane width in elements
+    long long off;           // element offset of this level inside a pair's class slab
+    long long class_elems;   // 4 * UH * PW
+};
+
+struct ClassPlan {
+    ClassLevel lv[kMaxLevels];
+    long long elems_per_pair;
+};
+
+struct LkClassArgs {
+    Geometry g;
+    ClassPlan plan;
+    const int16_t* rlist;    // [level][axis][128] class index -> residue
+    int level;
+};
+
 struct LkArgs {
     const uint8_t* pyr1;     // prev pyramid slabs
     const uint8_t* pyr2;     // next pyramid slabs
@@ -52,6 +74,11 @@ struct LkArgs {
     double eps2;
     float* next_pts;         // [batch][npts][2]
     uint8_t* status;         // [batch][npts]
+    ClassPlan plan;          // LK v2 only
+    const int16_t* cmap;     // [level][axis][128] residue -> class index
+    const int16_t* rlist;    // [level][axis][128] class index -> residue
+    float4* dbg;             // optional [batch][nlev][npts] (npx, npy, iters, status) at level end
+    int dbg_pt;              // point whose per-iteration values are appended after dbg (pair 0)
 };
 
 // Launchers (mdx_kernels.hip).  All enqueue on `s`.
@@ -61,6 +88,7 @@ hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const u
 hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level);
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level);
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
+hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint2* cls, float4* Abuf);
 hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
                                int ny, int pixel_step, double min_vector_size, double* vectors, PairFit* fits,
                                int fit_mode, const double* H_external);
