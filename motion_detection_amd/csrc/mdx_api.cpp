@@ -181,12 +181,12 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
             C.nrx = n[0];
             C.nry = n[1];
             C.UH = g.lv[l].h + 79;
-            C.PW = (g.lv[l].w + 82) / 4 + 4;
-            C.class_elems = 4LL * C.UH * C.PW;
+            C.PW = ((g.lv[l].w + 82) / 4 + 4 + 1) & ~1;
+            C.class_bytes = 4LL * C.UH * C.PW * 6;
             C.off = off;
-            off += (long long)C.nrx * C.nry * C.class_elems;
+            off += (long long)C.nrx * C.nry * C.class_bytes;
         }
-        P.elems_per_pair = (off + 31) / 32 * 32;
+        P.bytes_per_pair = (off + 255) / 256 * 256;
         if ((rc = ensure(c, c->ctab, tab.size() * sizeof(int16_t))) != MDX_OK) return rc;
         HIP_OR_RETURN(c, hipMemcpy(c->ctab.p, tab.data(), tab.size() * sizeof(int16_t), hipMemcpyHostToDevice));
         c->plan = P;
@@ -196,7 +196,7 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
         c->plan_ml = g.nlev;
     }
     const int npts = mdx_grid_count(w, h, ps);
-    if ((rc = ensure(c, c->cls, (size_t)c->plan.elems_per_pair * 8 * batch)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->cls, (size_t)c->plan.bytes_per_pair * batch + 64)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->Abuf, (size_t)npts * g.nlev * 16 * batch)) != MDX_OK) return rc;
     return MDX_OK;
 }
@@ -398,7 +398,7 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
                 const char* e = std::getenv("MDX_LK_DEBUG_PT");
                 a.dbg_pt = e ? std::atoi(e) : -1;
             }
-            HIP_OR_RETURN(c, launch_lk_v2(s, batch, a, c->cls.as<uint2>(), c->Abuf.as<float4>()));
+            HIP_OR_RETURN(c, launch_lk_v2(s, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>()));
         }
     }
     mark(c, 4);

@@ -41,18 +41,18 @@ struct PairFit {
 };
 
 // Residue-class planes of LK v2 (mdx_lk.hip): per level, one plane set per class of
-// (P_x mod 2^L, P_y mod 2^L) present in the grid.  Each class holds 4 planes (column mod 4)
-// of UH x PW elements; an element is uint2(Ix | Iy << 16, I*32).
+// (P_x mod 2^L, P_y mod 2^L) present in the grid.  Each class holds 4 D planes (column mod 4)
+// of UH x PW uint32 (Ix | Iy << 16) followed by 4 I planes of UH x PW int16 (I*32).
 struct ClassLevel {
     int nrx, nry;            // residue classes per axis
-    int UH, PW;              // plane rows (h + 79), plane width in elements
-    long long off;           // element offset of this level inside a pair's class slab
-    long long class_elems;   // 4 * UH * PW
+    int UH, PW;              // plane rows (h + 79), plane width in elements (even)
+    long long off;           // byte offset of this level inside a pair's class slab
+    long long class_bytes;   // 4 * UH * PW * (4 + 2)
 };
 
 struct ClassPlan {
     ClassLevel lv[kMaxLevels];
-    long long elems_per_pair;
+    long long bytes_per_pair;
 };
 
 struct LkClassArgs {
@@ -88,7 +88,7 @@ hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const u
 hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level);
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level);
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
-hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint2* cls, float4* Abuf);
+hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint8_t* cls, float4* Abuf);
 hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
                                int ny, int pixel_step, double min_vector_size, double* vectors, PairFit* fits,
                                int fit_mode, const double* H_external);

@@ -33,6 +33,7 @@ typedef short s2 __attribute__((ext_vector_type(2)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef uint4 __attribute__((aligned(8))) uint4_a8;
 typedef uint4 __attribute__((aligned(4))) uint4_a4;
+typedef uint2 __attribute__((aligned(4))) uint2_a4;
 
 // residue-class tables: [level][axis][128]
 __device__ __forceinline__ int class_of(const int16_t* cmap, int level, int axis, int res)
@@ -66,7 +67,7 @@ __device__ __forceinline__ float quad_bcast(float v)
 // (x, y) = (u - 40, v - 40) for the class's bilinear weights: (I*32, Ix, Iy) exactly as
 // LKTrackerInvoker extracts them (CV_DESCALE by W_BITS1-5 = 9 and W_BITS1 = 14).
 __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ pyr1, const uint32_t* __restrict__ der,
-                                                  uint2* __restrict__ cls_out, LkClassArgs a)
+                                                  uint8_t* __restrict__ cls_out, LkClassArgs a)
 {
     const int level = a.level;
     const ClassLevel& C = a.plan.lv[level];
@@ -86,11 +87,14 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
     const uint32_t* D = der + (long long)pair * a.g.der_words + L.der_off + L.core();
     const int y = v - kPad;
     const int p = L.pitch;
-    uint2* out = cls_out + (long long)pair * a.plan.elems_per_pair + C.off + (long long)cls * C.class_elems;
+    uint8_t* base = cls_out + (long long)pair * a.plan.bytes_per_pair + C.off + (long long)cls * C.class_bytes;
+    uint32_t* Dout = reinterpret_cast<uint32_t*>(base);
+    uint16_t* Iout = reinterpret_cast<uint16_t*>(base + 16LL * C.UH * C.PW);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int x = 4 * j + q - kPad;
-        uint2 e = make_uint2(0u, 0u);
+        uint32_t dv = 0;
+        uint16_t iv = 0;
         if (x < L.w + kPad - 1 && y < L.h + kPad - 1) {
             const uint8_t* ip = I + (long long)y * p + x;
             const int ival = (ip[0] * w00 + ip[1] * w01 + ip[p] * w10 + ip[p + 1] * w11 + 256) >> 9;
@@ -100,22 +104,47 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
                              (int)(int16_t)d11 * w11 + 8192) >> 14;
             const int iyv = (((int)d00 >> 16) * w00 + ((int)d01 >> 16) * w01 + ((int)d10 >> 16) * w10 +
                              ((int)d11 >> 16) * w11 + 8192) >> 14;
-            e.x = ((uint32_t)ixv & 0xffffu) | ((uint32_t)iyv << 16);
-            e.y = (uint32_t)ival;
+            dv = ((uint32_t)ixv & 0xffffu) | ((uint32_t)iyv << 16);
+            iv = (uint16_t)ival;
         }
-        out[((long long)q * C.UH + v) * C.PW + j] = e;
+        const long long o = ((long long)q * C.UH + v) * C.PW + j;
+        Dout[o] = dv;
+        Iout[o] = iv;
     }
+}
+
+// Point of lane `lane` in wave `w`: each wave takes 16 consecutive grid columns of ONE grid row
+// (same iy), so at every window row the 64 lanes read the same image rows -> coalesced loads.
+// XCD-aware block order: blocks are dealt round-robin over the 8 XCDs; remap so that each
+// XCD gets a contiguous range of waves (= a contiguous image band), whose class planes then
+// stay in that XCD's L2.  Bijective for any count (cdna_hip_programming.md §5.5 T1).
+__device__ __forceinline__ int xcd_remap(int b, int total)
+{
+    const int xcd = b & 7, q = total >> 3, r = total & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+__device__ __forceinline__ void wave_point(const LkArgs& a, int w, int lane, int& pt, int& gx, int& gy, bool& valid)
+{
+    const int nx = (a.npts + a.ny - 1) / a.ny;
+    gy = w % a.ny;
+    gx = (w / a.ny) * 16 + (lane >> 2);
+    valid = gx < nx;
+    pt = gx * a.ny + gy;
+    if (!valid) { gx = 0; pt = 0; }
 }
 
 // Window origin, class and plane addressing shared by k_lk_A and k_lk_track.
 struct WinRef {
     bool ok;
     int ipx, ipy;
-    const uint2* row0;   // this lane's chain start in row 0 of the window
-    int PW;
+    const uint32_t* drow;   // this lane's chain start (D plane) in row 0 of the window
+    const uint32_t* irow;   // 4-B aligned word holding its first I value (I plane)
+    int ishift;             // 0 or 16: bit offset of the first I value in *irow
+    int dstride, istride;   // row strides in words
 };
 
-__device__ __forceinline__ WinRef win_ref(const LkArgs& a, const uint2* cls, int pair, int level, int gx, int gy,
+__device__ __forceinline__ WinRef win_ref(const LkArgs& a, const uint8_t* cls, int pair, int level, int gx, int gy,
                                           float px0, float py0, int k, bool valid)
 {
     WinRef r;
@@ -126,59 +155,61 @@ __device__ __forceinline__ WinRef win_ref(const LkArgs& a, const uint2* cls, int
     r.ipx = (int)floorf(ppx);
     r.ipy = (int)floorf(ppy);
     r.ok = valid && !(r.ipx < -kWin || r.ipx >= L.w || r.ipy < -kWin || r.ipy >= L.h);
-    r.PW = C.PW;
+    r.dstride = C.PW;
+    r.istride = C.PW >> 1;
     // lanes without a window read class 0, plane 0 from its origin (always in bounds) so that
     // the chain loops run wave-uniform; their sums are discarded.
-    r.row0 = cls + (long long)pair * a.plan.elems_per_pair + C.off;
+    const uint8_t* base = cls + (long long)pair * a.plan.bytes_per_pair + C.off;
+    long long eo = 0;
     if (r.ok) {
         const int m = (1 << level) - 1;
         const int cx = class_of(a.cmap, level, 0, (gx * a.pixel_step) & m);
         const int cy = class_of(a.cmap, level, 1, (gy * a.pixel_step) & m);
         const int u = r.ipx + kPad + k;
         const int q = u & 3, j0 = u >> 2;
-        r.row0 = cls + (long long)pair * a.plan.elems_per_pair + C.off + (long long)(cy * C.nrx + cx) * C.class_elems +
-                 ((long long)q * C.UH + (r.ipy + kPad)) * C.PW + j0;
+        base += (long long)(cy * C.nrx + cx) * C.class_bytes;
+        eo = ((long long)q * C.UH + (r.ipy + kPad)) * C.PW + j0;
     }
+    r.drow = reinterpret_cast<const uint32_t*>(base) + eo;
+    r.irow = reinterpret_cast<const uint32_t*>(base + 16LL * C.UH * C.PW) + (eo >> 1);
+    r.ishift = (int)(eo & 1) * 16;
     return r;
 }
 
 // ------------------------------------------------------------------ A sums
 // grid: x -> 16 points per 64-lane wave, y -> level, z -> pair.  Output per (pair, level,
 // point): float4(A11, A12, A22, ok) with the FLT_SCALE already applied.
-__global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint2* __restrict__ cls, float4* __restrict__ Aout)
+__global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict__ cls, float4* __restrict__ Aout)
 {
     const int lane = threadIdx.x, k = lane & 3;
-    const int pt = blockIdx.x * 16 + (lane >> 2);
-    const int level = blockIdx.y, pair = blockIdx.z;
-    const bool valid = pt < a.npts;
-    const int gx = valid ? pt / a.ny : 0, gy = valid ? pt % a.ny : 0;
+    const int nw = gridDim.x, total = nw * gridDim.y * gridDim.z;
+    const int bid = xcd_remap(blockIdx.x + nw * (blockIdx.y + gridDim.y * blockIdx.z), total);
+    const int level = (bid / nw) % gridDim.y, pair = bid / (nw * gridDim.y);
+    int pt, gx, gy;
+    bool valid;
+    wave_point(a, bid % nw, lane, pt, gx, gy, valid);
     const WinRef r = win_ref(a, cls, pair, level, gx, gy, (float)(gx * a.pixel_step), (float)(gy * a.pixel_step), k,
                              valid);
-    float s11 = 0.f, s12 = 0.f, s22 = 0.f;
-    {
-        f2 sd = {0.f, 0.f};
-        const uint2* rp = r.row0;
-        for (int y = 0; y < kWin; y++, rp += r.PW) {
-            uint2 e[10];
-            const uint4_a8* v4 = reinterpret_cast<const uint4_a8*>(rp);
+    f2 sd = {0.f, 0.f};
+    float s12 = 0.f;
+    const uint32_t* dp = r.drow;
+    for (int y = 0; y < kWin; y++, dp += r.dstride) {
+        uint32_t d[10];
+        const uint4_a4* v4 = reinterpret_cast<const uint4_a4*>(dp);
+        const uint4 w0 = v4[0], w1 = v4[1];
+        const uint2 w2 = *reinterpret_cast<const uint2_a4*>(dp + 8);
+        d[0] = w0.x; d[1] = w0.y; d[2] = w0.z; d[3] = w0.w;
+        d[4] = w1.x; d[5] = w1.y; d[6] = w1.z; d[7] = w1.w;
+        d[8] = w2.x; d[9] = w2.y;
 #pragma unroll
-            for (int t = 0; t < 5; t++) {
-                const uint4 w = v4[t];
-                e[2 * t] = make_uint2(w.x, w.y);
-                e[2 * t + 1] = make_uint2(w.z, w.w);
-            }
-#pragma unroll
-            for (int g = 0; g < 10; g++) {
-                const uint32_t d = e[g].x;
-                const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
-                sd = sd + f * f;                 // (Ix*Ix, Iy*Iy)
-                s12 = s12 + f.x * f.y;           // Ix*Iy
-            }
+        for (int g = 0; g < 10; g++) {
+            const f2 f = {(float)(int16_t)d[g], (float)((int)d[g] >> 16)};
+            sd = sd + f * f;                 // (Ix*Ix, Iy*Iy)
+            s12 = s12 + f.x * f.y;           // Ix*Iy
         }
-        s11 = r.ok ? sd.x : 0.f;
-        s22 = r.ok ? sd.y : 0.f;
-        s12 = r.ok ? s12 : 0.f;
     }
+    const float s11 = r.ok ? sd.x : 0.f, s22 = r.ok ? sd.y : 0.f;
+    s12 = r.ok ? s12 : 0.f;
     // ((P0+P1)+P2)+P3 across the quad (SSE lanes 0..3)
     const float a11 = ((quad_bcast<0>(s11) + quad_bcast<1>(s11)) + quad_bcast<2>(s11)) + quad_bcast<3>(s11);
     const float a12 = ((quad_bcast<0>(s12) + quad_bcast<1>(s12)) + quad_bcast<2>(s12)) + quad_bcast<3>(s12);
@@ -191,15 +222,17 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint2* __restrict__
 }
 
 // ------------------------------------------------------------------ tracking
-__global__ __launch_bounds__(64) void k_lk_track(LkArgs a, const uint2* __restrict__ cls, const float4* __restrict__ Ain)
+__global__ __launch_bounds__(64) void k_lk_track(LkArgs a, const uint8_t* __restrict__ cls, const float4* __restrict__ Ain)
 {
     constexpr float HALFW = 19.5f;
     constexpr float FLT_SCALE = 1.f / (1 << 20);
     const int lane = threadIdx.x, k = lane & 3;
-    const int pt = blockIdx.x * 16 + (lane >> 2);
-    const int pair = blockIdx.y;
-    const bool valid = pt < a.npts;
-    const int gx = valid ? pt / a.ny : 0, gy = valid ? pt % a.ny : 0;
+    const int nw = gridDim.x;
+    const int bid = xcd_remap(blockIdx.x + nw * blockIdx.y, nw * gridDim.y);
+    const int pair = bid / nw;
+    int pt, gx, gy;
+    bool valid;
+    wave_point(a, bid % nw, lane, pt, gx, gy, valid);
     const float px0 = (float)(gx * a.pixel_step), py0 = (float)(gy * a.pixel_step);
     float npx = 0.f, npy = 0.f;
     int status = 1;
@@ -267,8 +300,9 @@ __global__ __launch_bounds__(64) void k_lk_track(LkArgs a, const uint2* __restri
                     r0[4 * t] = w.x; r0[4 * t + 1] = w.y; r0[4 * t + 2] = w.z; r0[4 * t + 3] = w.w;
                 }
             }
-            const uint2* rp = r.row0;
-            for (int y = 0; y < kWin; y++, rp += r.PW) {
+            const uint32_t* dp = r.drow;
+            const uint32_t* ip = r.irow;
+            for (int y = 0; y < kWin; y++, dp += r.dstride, ip += r.istride) {
                 jrow += jstride;
                 const uint4_a4* p4 = reinterpret_cast<const uint4_a4*>(jrow);
 #pragma unroll
@@ -276,22 +310,28 @@ __global__ __launch_bounds__(64) void k_lk_track(LkArgs a, const uint2* __restri
                     const uint4 w = p4[t];
                     r1[4 * t] = w.x; r1[4 * t + 1] = w.y; r1[4 * t + 2] = w.z; r1[4 * t + 3] = w.w;
                 }
-                uint2 e[10];
-                const uint4_a8* v4 = reinterpret_cast<const uint4_a8*>(rp);
+                uint32_t d[10], iw[6], iv[5];
+                {
+                    const uint4_a4* v4 = reinterpret_cast<const uint4_a4*>(dp);
+                    const uint4 w0 = v4[0], w1 = v4[1];
+                    const uint2 w2 = *reinterpret_cast<const uint2_a4*>(dp + 8);
+                    d[0] = w0.x; d[1] = w0.y; d[2] = w0.z; d[3] = w0.w;
+                    d[4] = w1.x; d[5] = w1.y; d[6] = w1.z; d[7] = w1.w;
+                    d[8] = w2.x; d[9] = w2.y;
+                    const uint4 u0 = *reinterpret_cast<const uint4_a4*>(ip);
+                    const uint2 u1 = *reinterpret_cast<const uint2_a4*>(ip + 4);
+                    iw[0] = u0.x; iw[1] = u0.y; iw[2] = u0.z; iw[3] = u0.w; iw[4] = u1.x; iw[5] = u1.y;
 #pragma unroll
-                for (int t = 0; t < 5; t++) {
-                    const uint4 w = v4[t];
-                    e[2 * t] = make_uint2(w.x, w.y);
-                    e[2 * t + 1] = make_uint2(w.z, w.w);
+                    for (int t = 0; t < 5; t++) iv[t] = __builtin_amdgcn_alignbit(iw[t + 1], iw[t], r.ishift);
                 }
 #pragma unroll
                 for (int g = 0; g < 10; g++) {
                     const s2 pa = __builtin_bit_cast(s2, __builtin_amdgcn_perm(r0[g + 1], r0[g], sel));
                     const s2 pb = __builtin_bit_cast(s2, __builtin_amdgcn_perm(r1[g + 1], r1[g], sel));
                     const int jv = __builtin_amdgcn_sdot2(pa, W0, __builtin_amdgcn_sdot2(pb, W1, 256, false), false) >> 9;
-                    const float fd = (float)(jv - (int)e[g].y);
-                    const uint32_t d = e[g].x;
-                    const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
+                    const int ival = (g & 1) ? (int)(iv[g >> 1] >> 16) : (int)(iv[g >> 1] & 0xffffu);
+                    const float fd = (float)(jv - ival);
+                    const f2 f = {(float)(int16_t)d[g], (float)((int)d[g] >> 16)};
                     acc = acc + f * fd;
                 }
 #pragma unroll
@@ -340,7 +380,7 @@ __global__ __launch_bounds__(64) void k_lk_track(LkArgs a, const uint2* __restri
     }
 }
 
-hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint2* cls, float4* Abuf)
+hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint8_t* cls, float4* Abuf)
 {
     for (int l = 0; l <= a.maxl; l++) {
         const ClassLevel& C = a.plan.lv[l];
@@ -352,8 +392,10 @@ hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint2* cls, f
         const dim3 grid((C.PW + 63) / 64, C.UH, batch * C.nrx * C.nry);
         hipLaunchKernelGGL(k_lk_class, grid, dim3(64), 0, s, a.pyr1, a.der, cls, ca);
     }
-    hipLaunchKernelGGL(k_lk_A, dim3((a.npts + 15) / 16, a.maxl + 1, batch), dim3(64), 0, s, a, cls, Abuf);
-    hipLaunchKernelGGL(k_lk_track, dim3((a.npts + 15) / 16, batch), dim3(64), 0, s, a, cls, Abuf);
+    const int nx = (a.npts + a.ny - 1) / a.ny;
+    const int nwaves = ((nx + 15) / 16) * a.ny;
+    hipLaunchKernelGGL(k_lk_A, dim3(nwaves, a.maxl + 1, batch), dim3(64), 0, s, a, cls, Abuf);
+    hipLaunchKernelGGL(k_lk_track, dim3(nwaves, batch), dim3(64), 0, s, a, cls, Abuf);
     return hipGetLastError();
 }
 
