@@ -12,6 +12,9 @@ import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmdx.so")
+# developer hook: load an alternative build (e.g. scripts/lk_variants.sh timing-only variants)
+if os.environ.get("MDX_LIB_PATH"):
+    LIB_PATH = os.environ["MDX_LIB_PATH"]
 CSRC = os.path.join(_HERE, "csrc")
 
 MDX_OK = 0

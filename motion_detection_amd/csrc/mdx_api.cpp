@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 #include <cstdlib>
+#include <cmath>
 
 using namespace mdx;
 
@@ -148,8 +149,10 @@ static int ensure_workspace(mdx_ctx* c, const Geometry& g, int batch)
     return MDX_OK;
 }
 
-// Residue classes of the grid at each level (see mdx_lk.hip) and the class-plane layout.
-// Tables are rebuilt and uploaded only when the frame size / pixel_step / level count change.
+// Residue classes of the grid at each level (see mdx_lk.hip), the class-grouped point order and
+// the class-plane layout.  Rebuilt and uploaded only when frame size / pixel_step / levels change.
+// plan.nch == 0 means the 8-point union of some group is wider than 512 columns (pixel_step >~ 66):
+// the caller then runs the single-kernel LK instead.
 static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps, int batch)
 {
     int rc;
@@ -157,10 +160,11 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
         const int nx = (w + ps - 1) / ps, ny = (h + ps - 1) / ps;
         static_assert(kMaxLevels <= 8, "residue tables sized for 2^7 residues");
         std::vector<int16_t> tab(2 * kMaxLevels * 2 * 128, (int16_t)-1);
+        std::vector<int16_t> ord;
         int16_t* cmap = tab.data();
         int16_t* rlist = tab.data() + kMaxLevels * 2 * 128;
         ClassPlan P{};
-        long long off = 0;
+        int umax = 0;
         for (int l = 0; l < g.nlev; l++) {
             const int m = (1 << l) - 1;
             int n[2] = {0, 0};
@@ -180,13 +184,42 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
             ClassLevel& C = P.lv[l];
             C.nrx = n[0];
             C.nry = n[1];
+            // columns: each class's members in x order, the run padded to a multiple of 8 (-1)
+            C.ord_off = (int)ord.size();
+            const int16_t* cmx = cmap + (l * 2 + 0) * 128;
+            const float scale = (float)(1. / (1 << l));
+            auto ipx_of = [&](int gx) { return (int)std::floor((float)(gx * ps) * scale - 19.5f); };
+            for (int cls = 0; cls < n[0]; cls++) {
+                const size_t run0 = ord.size();
+                for (int i = 0; i < nx; i++)
+                    if (cmx[(i * ps) & m] == cls) ord.push_back((int16_t)i);
+                for (size_t q = run0; q < ord.size(); q += 8) {    // union width of each 8-group
+                    const size_t last = std::min(ord.size(), q + 8) - 1;
+                    umax = std::max(umax, ipx_of(ord[last]) - ipx_of(ord[q]) + kWin);
+                }
+                while ((ord.size() - run0) % 8) ord.push_back((int16_t)-1);
+            }
+            C.nxp = (int)ord.size() - C.ord_off;
+            // rows: grouped by class the same way (no padding: a wave takes one row)
+            const size_t r0 = ord.size();
+            for (int i = 0; i < ny; i++) ord.push_back((int16_t)i);
+            const int16_t* cmy = cmap + (l * 2 + 1) * 128;
+            std::stable_sort(ord.begin() + r0, ord.end(),
+                             [&](int16_t u, int16_t v) { return cmy[(u * ps) & m] < cmy[(v * ps) & m]; });
+        }
+        P.nch = umax <= 128 ? 1 : umax <= 256 ? 2 : umax <= 512 ? 4 : 0;
+        const int UW = 128 * std::max(P.nch, 1);
+        long long off = 0;
+        for (int l = 0; l < g.nlev; l++) {
+            ClassLevel& C = P.lv[l];
             C.UH = g.lv[l].h + 79;
-            C.PW = ((g.lv[l].w + 82) / 4 + 4 + 1) & ~1;
-            C.class_bytes = 4LL * C.UH * C.PW * 6;
+            C.PW = (g.lv[l].w + kPad + UW + 3) & ~3;
+            C.class_bytes = (long long)C.UH * C.PW * 8;
             C.off = off;
             off += (long long)C.nrx * C.nry * C.class_bytes;
         }
         P.bytes_per_pair = (off + 255) / 256 * 256;
+        tab.insert(tab.end(), ord.begin(), ord.end());
         if ((rc = ensure(c, c->ctab, tab.size() * sizeof(int16_t))) != MDX_OK) return rc;
         HIP_OR_RETURN(c, hipMemcpy(c->ctab.p, tab.data(), tab.size() * sizeof(int16_t), hipMemcpyHostToDevice));
         c->plan = P;
@@ -195,9 +228,8 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
         c->plan_ps = ps;
         c->plan_ml = g.nlev;
     }
-    const int npts = mdx_grid_count(w, h, ps);
+    if (c->plan.nch == 0) return MDX_OK;
     if ((rc = ensure(c, c->cls, (size_t)c->plan.bytes_per_pair * batch + 64)) != MDX_OK) return rc;
-    if ((rc = ensure(c, c->Abuf, (size_t)npts * g.nlev * 16 * batch)) != MDX_OK) return rc;
     return MDX_OK;
 }
 
@@ -384,13 +416,18 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         a.eps2 = e * e;
         a.next_pts = d_np;
         a.status = d_st;
-        if (c->lk_impl == 1) {
+        bool v2 = c->lk_impl == 2;
+        if (v2) {
+            if ((rc = ensure_class_plan(c, g, w, h, P.pixel_step, batch)) != MDX_OK) return rc;
+            v2 = c->plan.nch != 0;   // very sparse grids: the single-kernel LK
+        }
+        if (!v2) {
             HIP_OR_RETURN(c, launch_lk(s, batch, a));
         } else {
-            if ((rc = ensure_class_plan(c, g, w, h, P.pixel_step, batch)) != MDX_OK) return rc;
             a.plan = c->plan;
             a.cmap = c->ctab.as<int16_t>();
             a.rlist = c->ctab.as<int16_t>() + kMaxLevels * 2 * 128;
+            a.ord = c->ctab.as<int16_t>() + 2 * kMaxLevels * 2 * 128;
             if (c->lk_debug) {
                 if ((rc = ensure(c, c->dbg, ((size_t)npts * g.nlev * batch + kMaxLevels * 64) * 16)) != MDX_OK)
                     return rc;
@@ -398,7 +435,7 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
                 const char* e = std::getenv("MDX_LK_DEBUG_PT");
                 a.dbg_pt = e ? std::atoi(e) : -1;
             }
-            HIP_OR_RETURN(c, launch_lk_v2(s, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>()));
+            HIP_OR_RETURN(c, launch_lk_v2(s, batch, a, c->cls.as<uint8_t>()));
         }
     }
     mark(c, 4);

@@ -41,18 +41,21 @@ struct PairFit {
 };
 
 // Residue-class planes of LK v2 (mdx_lk.hip): per level, one plane set per class of
-// (P_x mod 2^L, P_y mod 2^L) present in the grid.  Each class holds 4 D planes (column mod 4)
-// of UH x PW uint32 (Ix | Iy << 16) followed by 4 I planes of UH x PW int16 (I*32).
+// (P_x mod 2^L, P_y mod 2^L) present in the grid.  Each class holds two row-major UH x PW arrays:
+// D (uint32, Ix | Iy << 16) then C (int32, 256 - 512*I: the J-chain bias, see mdx_lk.hip).
 struct ClassLevel {
     int nrx, nry;            // residue classes per axis
-    int UH, PW;              // plane rows (h + 79), plane width in elements (even)
+    int UH, PW;              // plane rows (h + 79), plane width in elements (multiple of 4)
     long long off;           // byte offset of this level inside a pair's class slab
-    long long class_bytes;   // 4 * UH * PW * (4 + 2)
+    long long class_bytes;   // UH * PW * 8
+    int nxp;                 // length of the padded class-grouped column order (multiple of 8)
+    int ord_off;             // offset of this level's order tables in LkArgs::ord
 };
 
 struct ClassPlan {
     ClassLevel lv[kMaxLevels];
     long long bytes_per_pair;
+    int nch;                 // union chunks of 128 columns per 8-point group (1, 2 or 4)
 };
 
 struct LkClassArgs {
@@ -77,6 +80,8 @@ struct LkArgs {
     ClassPlan plan;          // LK v2 only
     const int16_t* cmap;     // [level][axis][128] residue -> class index
     const int16_t* rlist;    // [level][axis][128] class index -> residue
+    const int16_t* ord;      // per level: nxp padded grid columns (-1 = empty), then ny grid rows,
+                             // both grouped by residue class (ClassLevel::ord_off)
     float4* dbg;             // optional [batch][nlev][npts] (npx, npy, iters, status) at level end
     int dbg_pt;              // point whose per-iteration values are appended after dbg (pair 0)
 };
@@ -88,7 +93,7 @@ hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const u
 hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level);
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level);
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
-hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint8_t* cls, float4* Abuf);
+hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint8_t* cls);
 hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
                                int ny, int pixel_step, double min_vector_size, double* vectors, PairFit* fits,
                                int fit_mode, const double* H_external);

@@ -1,28 +1,38 @@
 // mdx_lk.hip -- pyramidal Lucas-Kanade (reference row A5: calcOpticalFlowPyrLK as called at
 // optical_flow_calculator.cpp:71), restructured for CDNA4 while keeping OpenCV 2.4's x86 SSE2
-// arithmetic bit for bit.
+// arithmetic bit for bit.  This is the "class plane" LK (MDX_LK_IMPL=2, default); the
+// single-kernel k_lk in mdx_kernels.hip is the general fallback.
 //
-// Three kernels per batch of frame pairs:
+// Per pyramid level, from maxLevel down to 0, two kernels:
 //
-//  k_lk_class  For every level and every fractional-offset class, the interpolated window
-//              values (I*32 descaled by 9 bits, Ix/Iy descaled by 14 bits) over the whole
-//              padded level.  At level L a grid point's window origin prevPt - 19.5 has a
-//              fractional part fixed by (P mod 2^L), so all points of a residue class share
-//              the bilinear weights: the 16x-overlapping per-window interpolation of the
-//              reference becomes one interpolation per class and pixel.  Stored de-interleaved
-//              by column mod 4 ("planes"), so the 10 elements of one SSE lane's chain in a
-//              window row are contiguous.
-//  k_lk_A      Per point and level, the gradient matrix sums A11/A12/A22.  They depend only on
-//              the original point and the level (not on tracking), so they are computed for all
-//              levels at once.  4 lanes per point: lane k owns the SSE lane k chain (window
-//              columns x = 4g+k, rows in order) and adds in registers; the four partials are
-//              combined ((P0+P1)+P2)+P3 across the lane quad.
-//  k_lk_track  Newton iterations level by level.  Same 4-lanes-per-point chain layout for
-//              b1/b2 (combined (P0+P2)+(P1+P3)); J taps via v_perm_b32 + v_dot2_u32_u16; the
-//              products are formed as float multiplies of exactly-converted integers (one
-//              rounding of the exact product == the reference's (float)(int product)).
+//  k_lk_class  The interpolated window values (I*32 descaled by 9 bits, Ix/Iy descaled by 14
+//              bits) over the whole padded level, once per fractional-offset class.  At level L a
+//              grid point's window origin prevPt - 19.5 has a fractional part fixed by
+//              (P mod 2^L), so all points of a residue class share the bilinear weights: the
+//              16x-overlapping per-window interpolation of the reference becomes one
+//              interpolation per class and pixel.  Natural row-major layout, two arrays per
+//              class: D = (Ix | Iy << 16) and C = 256 - 512*I (the J-chain bias, see below).
+//  k_lk_level  Per point: the gradient matrix sums A11/A12/A22 over the window, the minEig /
+//              determinant tests, then the Newton iterations.
 //
-// Products/sums never go through FMA (-ffp-contract=off).
+// Work mapping of k_lk_level.  A wave = 16 points x 4 lanes: lane k of a point owns SSE lane k
+// (window columns x = 4g + k, g = 0..9, rows in order) and keeps its partial sums in registers;
+// partials are combined across the lane quad in the reference's order (A: ((P0+P1)+P2)+P3,
+// b: (P0+P2)+(P1+P3)).  The 16 points of a wave are two groups of 8 consecutive members of one
+// residue class along one grid row (host-built class-grouped order, runs padded to 8), so a
+// group's windows share their rows and overlap in columns: per window row the group needs one
+// contiguous "union" segment of <= 128*NCH columns of D and C.  Each half-wave loads its
+// group's segment with one coalesced dwordx4 per array and lane, stores it to a double-buffered
+// LDS row, and every lane then reads its 10 chain elements with ds_read_b32.  That replaces the
+// 6 scattered dwordx2/x4 loads per lane and row that bound the previous design on the texture
+// data path (TD busy 97%, VALU 38%).  J (the moving window in the next frame) differs per point:
+// its row segment is loaded once per lane quad (3 dwords per lane) and shared by DPP.
+//
+// Arithmetic: J taps via v_perm_b32 + v_dot2_i32_i16 (signed weights: w11 may be -1);
+// dot2(pa, W0, dot2(pb, W1, C)) >> 9 == ((S + 256) >> 9) - I exactly, because C = 256 - 512*I
+// is a multiple-of-512 shift of the rounding bias.  Products are float multiplies of exactly
+// converted integers (one rounding of the exact product == the reference's (float)(int
+// product)).  Products/sums never go through FMA (-ffp-contract=off).
 #include "mdx_internal.h"
 
 #include <float.h>
@@ -31,9 +41,9 @@ namespace mdx {
 
 typedef short s2 __attribute__((ext_vector_type(2)));
 typedef float f2 __attribute__((ext_vector_type(2)));
-typedef uint4 __attribute__((aligned(8))) uint4_a8;
-typedef uint4 __attribute__((aligned(4))) uint4_a4;
-typedef uint2 __attribute__((aligned(4))) uint2_a4;
+// 4-B aligned multi-dword loads (global_load_dwordx4/x3 at dword-aligned addresses)
+struct __attribute__((aligned(4))) u4a4 { uint32_t x, y, z, w; };
+struct __attribute__((aligned(4))) u3a4 { uint32_t x, y, z; };
 
 // residue-class tables: [level][axis][128]
 __device__ __forceinline__ int class_of(const int16_t* cmap, int level, int axis, int res)
@@ -60,12 +70,40 @@ __device__ __forceinline__ float quad_bcast(float v)
     constexpr int ctrl = J | (J << 2) | (J << 4) | (J << 6);
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xf, 0xf, false));
 }
+template <int J>
+__device__ __forceinline__ uint32_t quad_bcast_u(uint32_t v)
+{
+    constexpr int ctrl = J | (J << 2) | (J << 4) | (J << 6);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xf, 0xf, false);
+}
+
+// One J row segment of a point's window, shared by its lane quad: the 11 dwords from the
+// 4-B aligned column B = inx & ~3 cover every lane's taps (lane k needs bytes o + 4g and
+// o + 4g + 1 with o = (inx & 3) + k <= 6, i.e. inside dwords g, g+1).  Each lane loads 3 of
+// them and DPP broadcasts assemble the row in every lane: 12 B of L1 traffic per lane, not 48.
+__device__ __forceinline__ void load_jrow_quad(const uint32_t* seg, int k, uint32_t (&r)[11])
+{
+    const u3a4 m = *reinterpret_cast<const u3a4*>(seg + 3 * k);
+    r[0] = quad_bcast_u<0>(m.x); r[1] = quad_bcast_u<0>(m.y); r[2] = quad_bcast_u<0>(m.z);
+    r[3] = quad_bcast_u<1>(m.x); r[4] = quad_bcast_u<1>(m.y); r[5] = quad_bcast_u<1>(m.z);
+    r[6] = quad_bcast_u<2>(m.x); r[7] = quad_bcast_u<2>(m.y); r[8] = quad_bcast_u<2>(m.z);
+    r[9] = quad_bcast_u<3>(m.x); r[10] = quad_bcast_u<3>(m.y);
+}
+
+// XCD-aware block order: blocks are dealt round-robin over the 8 XCDs; remap so that each
+// XCD gets a contiguous range of waves (= a contiguous image band), whose class planes then
+// stay in that XCD's L2.  Bijective for any count (cdna_hip_programming.md §5.5 T1).
+__device__ __forceinline__ int xcd_remap(int b, int total)
+{
+    const int xcd = b & 7, q = total >> 3, r = total & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
 
 // ------------------------------------------------------------------ class planes
-// grid: x -> plane column j (elements u = 4j..4j+3, one per plane), y -> plane row v,
-// z -> pair * nclass + class.  Element (u, v) is the window value at level core position
-// (x, y) = (u - 40, v - 40) for the class's bilinear weights: (I*32, Ix, Iy) exactly as
-// LKTrackerInvoker extracts them (CV_DESCALE by W_BITS1-5 = 9 and W_BITS1 = 14).
+// grid: x -> 4 consecutive plane columns u per thread, y -> plane row v, z -> pair * nclass +
+// class.  Element (u, v) is the window value at level core position (x, y) = (u - 40, v - 40)
+// for the class's bilinear weights: (I*32, Ix, Iy) exactly as LKTrackerInvoker extracts them
+// (CV_DESCALE by W_BITS1-5 = 9 and W_BITS1 = 14).  Outside the level's padded extent: 0.
 __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ pyr1, const uint32_t* __restrict__ der,
                                                   uint8_t* __restrict__ cls_out, LkClassArgs a)
 {
@@ -75,7 +113,7 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
     const int pair = blockIdx.z / nclass, cls = blockIdx.z % nclass;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int v = blockIdx.y;
-    if (j >= C.PW || v >= C.UH) return;
+    if (4 * j >= C.PW || v >= C.UH) return;
     const Level L = a.g.lv[level];
     const float scale = (float)(1. / (1 << level));
     const int rx = residue_of(a.rlist, level, 0, cls % C.nrx), ry = residue_of(a.rlist, level, 1, cls / C.nrx);
@@ -88,314 +126,289 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
     const int y = v - kPad;
     const int p = L.pitch;
     uint8_t* base = cls_out + (long long)pair * a.plan.bytes_per_pair + C.off + (long long)cls * C.class_bytes;
-    uint32_t* Dout = reinterpret_cast<uint32_t*>(base);
-    uint16_t* Iout = reinterpret_cast<uint16_t*>(base + 16LL * C.UH * C.PW);
+    uint32_t dv[4];
+    int cv[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int x = 4 * j + q - kPad;
-        uint32_t dv = 0;
-        uint16_t iv = 0;
+        dv[q] = 0;
+        int ival = 0;
         if (x < L.w + kPad - 1 && y < L.h + kPad - 1) {
             const uint8_t* ip = I + (long long)y * p + x;
-            const int ival = (ip[0] * w00 + ip[1] * w01 + ip[p] * w10 + ip[p + 1] * w11 + 256) >> 9;
+            ival = (ip[0] * w00 + ip[1] * w01 + ip[p] * w10 + ip[p + 1] * w11 + 256) >> 9;
             const uint32_t* dp = D + (long long)y * p + x;
             const uint32_t d00 = dp[0], d01 = dp[1], d10 = dp[p], d11 = dp[p + 1];
             const int ixv = ((int)(int16_t)d00 * w00 + (int)(int16_t)d01 * w01 + (int)(int16_t)d10 * w10 +
                              (int)(int16_t)d11 * w11 + 8192) >> 14;
             const int iyv = (((int)d00 >> 16) * w00 + ((int)d01 >> 16) * w01 + ((int)d10 >> 16) * w10 +
                              ((int)d11 >> 16) * w11 + 8192) >> 14;
-            dv = ((uint32_t)ixv & 0xffffu) | ((uint32_t)iyv << 16);
-            iv = (uint16_t)ival;
+            dv[q] = ((uint32_t)ixv & 0xffffu) | ((uint32_t)iyv << 16);
         }
-        const long long o = ((long long)q * C.UH + v) * C.PW + j;
-        Dout[o] = dv;
-        Iout[o] = iv;
+        cv[q] = 256 - 512 * ival;   // J-chain bias: (S + C) >> 9 == ((S + 256) >> 9) - I
     }
+    const long long o = (long long)v * C.PW + 4 * j;
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(base) + o) = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+    *reinterpret_cast<int4*>(reinterpret_cast<int32_t*>(base) + (long long)C.UH * C.PW + o) =
+        make_int4(cv[0], cv[1], cv[2], cv[3]);
 }
 
-// Point of lane `lane` in wave `w`: each wave takes 16 consecutive grid columns of ONE grid row
-// (same iy), so at every window row the 64 lanes read the same image rows -> coalesced loads.
-// XCD-aware block order: blocks are dealt round-robin over the 8 XCDs; remap so that each
-// XCD gets a contiguous range of waves (= a contiguous image band), whose class planes then
-// stay in that XCD's L2.  Bijective for any count (cdna_hip_programming.md §5.5 T1).
-__device__ __forceinline__ int xcd_remap(int b, int total)
+// ------------------------------------------------------------------ one pyramid level
+// grid: x -> wave (16 points), y -> pair (XCD-remapped as one linear range).  Levels run as
+// separate launches from maxLevel down to 0; the position carried between them is next_pts
+// (the reference's nextPts[ptidx], stored every level).
+template <int NCH>
+__global__ __launch_bounds__(64) void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
 {
-    const int xcd = b & 7, q = total >> 3, r = total & 7;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-}
-
-__device__ __forceinline__ void wave_point(const LkArgs& a, int w, int lane, int& pt, int& gx, int& gy, bool& valid)
-{
-    const int nx = (a.npts + a.ny - 1) / a.ny;
-    gy = w % a.ny;
-    gx = (w / a.ny) * 16 + (lane >> 2);
-    valid = gx < nx;
-    pt = gx * a.ny + gy;
-    if (!valid) { gx = 0; pt = 0; }
-}
-
-// Window origin, class and plane addressing shared by k_lk_A and k_lk_track.
-struct WinRef {
-    bool ok;
-    int ipx, ipy;
-    const uint32_t* drow;   // this lane's chain start (D plane) in row 0 of the window
-    const uint32_t* irow;   // 4-B aligned word holding its first I value (I plane)
-    int ishift;             // 0 or 16: bit offset of the first I value in *irow
-    int dstride, istride;   // row strides in words
-};
-
-__device__ __forceinline__ WinRef win_ref(const LkArgs& a, const uint8_t* cls, int pair, int level, int gx, int gy,
-                                          float px0, float py0, int k, bool valid)
-{
-    WinRef r;
-    const Level L = a.g.lv[level];
-    const ClassLevel& C = a.plan.lv[level];
-    const float scale = (float)(1. / (1 << level));
-    const float ppx = px0 * scale - 19.5f, ppy = py0 * scale - 19.5f;
-    r.ipx = (int)floorf(ppx);
-    r.ipy = (int)floorf(ppy);
-    r.ok = valid && !(r.ipx < -kWin || r.ipx >= L.w || r.ipy < -kWin || r.ipy >= L.h);
-    r.dstride = C.PW;
-    r.istride = C.PW >> 1;
-    // lanes without a window read class 0, plane 0 from its origin (always in bounds) so that
-    // the chain loops run wave-uniform; their sums are discarded.
-    const uint8_t* base = cls + (long long)pair * a.plan.bytes_per_pair + C.off;
-    long long eo = 0;
-    if (r.ok) {
-        const int m = (1 << level) - 1;
-        const int cx = class_of(a.cmap, level, 0, (gx * a.pixel_step) & m);
-        const int cy = class_of(a.cmap, level, 1, (gy * a.pixel_step) & m);
-        const int u = r.ipx + kPad + k;
-        const int q = u & 3, j0 = u >> 2;
-        base += (long long)(cy * C.nrx + cx) * C.class_bytes;
-        eo = ((long long)q * C.UH + (r.ipy + kPad)) * C.PW + j0;
-    }
-    r.drow = reinterpret_cast<const uint32_t*>(base) + eo;
-    r.irow = reinterpret_cast<const uint32_t*>(base + 16LL * C.UH * C.PW) + (eo >> 1);
-    r.ishift = (int)(eo & 1) * 16;
-    return r;
-}
-
-// ------------------------------------------------------------------ A sums
-// grid: x -> 16 points per 64-lane wave, y -> level, z -> pair.  Output per (pair, level,
-// point): float4(A11, A12, A22, ok) with the FLT_SCALE already applied.
-__global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict__ cls, float4* __restrict__ Aout)
-{
-    const int lane = threadIdx.x, k = lane & 3;
-    const int nw = gridDim.x, total = nw * gridDim.y * gridDim.z;
-    const int bid = xcd_remap(blockIdx.x + nw * (blockIdx.y + gridDim.y * blockIdx.z), total);
-    const int level = (bid / nw) % gridDim.y, pair = bid / (nw * gridDim.y);
-    int pt, gx, gy;
-    bool valid;
-    wave_point(a, bid % nw, lane, pt, gx, gy, valid);
-    const WinRef r = win_ref(a, cls, pair, level, gx, gy, (float)(gx * a.pixel_step), (float)(gy * a.pixel_step), k,
-                             valid);
-    f2 sd = {0.f, 0.f};
-    float s12 = 0.f;
-    const uint32_t* dp = r.drow;
-    for (int y = 0; y < kWin; y++, dp += r.dstride) {
-        uint32_t d[10];
-        const uint4_a4* v4 = reinterpret_cast<const uint4_a4*>(dp);
-        const uint4 w0 = v4[0], w1 = v4[1];
-        const uint2 w2 = *reinterpret_cast<const uint2_a4*>(dp + 8);
-        d[0] = w0.x; d[1] = w0.y; d[2] = w0.z; d[3] = w0.w;
-        d[4] = w1.x; d[5] = w1.y; d[6] = w1.z; d[7] = w1.w;
-        d[8] = w2.x; d[9] = w2.y;
-#pragma unroll
-        for (int g = 0; g < 10; g++) {
-            const f2 f = {(float)(int16_t)d[g], (float)((int)d[g] >> 16)};
-            sd = sd + f * f;                 // (Ix*Ix, Iy*Iy)
-            s12 = s12 + f.x * f.y;           // Ix*Iy
-        }
-    }
-    const float s11 = r.ok ? sd.x : 0.f, s22 = r.ok ? sd.y : 0.f;
-    s12 = r.ok ? s12 : 0.f;
-    // ((P0+P1)+P2)+P3 across the quad (SSE lanes 0..3)
-    const float a11 = ((quad_bcast<0>(s11) + quad_bcast<1>(s11)) + quad_bcast<2>(s11)) + quad_bcast<3>(s11);
-    const float a12 = ((quad_bcast<0>(s12) + quad_bcast<1>(s12)) + quad_bcast<2>(s12)) + quad_bcast<3>(s12);
-    const float a22 = ((quad_bcast<0>(s22) + quad_bcast<1>(s22)) + quad_bcast<2>(s22)) + quad_bcast<3>(s22);
-    if (valid && k == 0) {
-        const float FS = 1.f / (1 << 20);
-        Aout[((long long)pair * a.g.nlev + level) * a.npts + pt] =
-            make_float4(a11 * FS, a12 * FS, a22 * FS, r.ok ? 1.f : 0.f);
-    }
-}
-
-// ------------------------------------------------------------------ tracking
-__global__ __launch_bounds__(64) void k_lk_track(LkArgs a, const uint8_t* __restrict__ cls, const float4* __restrict__ Ain)
-{
+    constexpr int UW = NCH * 128;           // union columns per group
     constexpr float HALFW = 19.5f;
     constexpr float FLT_SCALE = 1.f / (1 << 20);
-    const int lane = threadIdx.x, k = lane & 3;
+    // [buf][group][D, C][UW]: a window row's union segment, double-buffered across rows
+    __shared__ __attribute__((aligned(16))) uint32_t lds[2][2][2][UW];
+
+    const int lane = threadIdx.x, k = lane & 3, grp = lane >> 5, gl = lane & 31;
     const int nw = gridDim.x;
     const int bid = xcd_remap(blockIdx.x + nw * blockIdx.y, nw * gridDim.y);
-    const int pair = bid / nw;
-    int pt, gx, gy;
-    bool valid;
-    wave_point(a, bid % nw, lane, pt, gx, gy, valid);
-    const float px0 = (float)(gx * a.pixel_step), py0 = (float)(gy * a.pixel_step);
-    float npx = 0.f, npy = 0.f;
-    int status = 1;
-    const uint8_t* slab2 = a.pyr2 + (long long)pair * a.g.img_bytes;
+    const int pair = bid / nw, w = bid % nw;
+    const ClassLevel& C = a.plan.lv[level];
+    const Level L = a.g.lv[level];
+    const int16_t* xo = a.ord + C.ord_off;
+    const int16_t* yo = xo + C.nxp;
+    const int slot = (w / a.ny) * 16 + (lane >> 2);
+    const int gxv = slot < C.nxp ? xo[slot] : -1;
+    const bool valid = gxv >= 0;
+    const int gx = valid ? gxv : 0, gy = yo[w % a.ny];
+    const int pt = gx * a.ny + gy;
+    const long long po = (long long)pair * a.npts + pt;
 
-    for (int level = a.maxl; level >= 0; --level) {
-        const Level L = a.g.lv[level];
-        const int pitch = L.pitch;
-        const uint8_t* Jb = slab2 + L.img_off + L.core();
-        const float scale = (float)(1. / (1 << level));
-        const float ppx = px0 * scale, ppy = py0 * scale;
-        if (level == a.maxl) { npx = ppx; npy = ppy; }
-        else { npx = npx * 2.f; npy = npy * 2.f; }
-        const WinRef r = win_ref(a, cls, pair, level, gx, gy, px0, py0, k, valid);
-        bool ok = r.ok;
-        if (valid && !ok && level == 0) status = 0;
-        float A11 = 0.f, A12 = 0.f, A22 = 0.f, Dinv = 0.f;
-        if (ok) {
-            const float4 A = Ain[((long long)pair * a.g.nlev + level) * a.npts + pt];
-            A11 = A.x; A12 = A.y; A22 = A.z;
-            const float D = A11 * A22 - A12 * A12;
-            const float minEig = (A22 + A11 - __builtin_sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
-                                 (float)(2 * kWin * kWin);
-            if (minEig < a.min_eig || D < FLT_EPSILON) {
-                ok = false;
-                if (level == 0) status = 0;
-            } else {
-                Dinv = 1.f / D;
-            }
-        }
-        float nx = npx - HALFW, ny = npy - HALFW;
-        float pdx = 0.f, pdy = 0.f;
-        bool act = ok;
-        int iters = 0;
-        for (int j = 0; j < a.max_iters; j++) {
-            if (!__any(act)) break;
-            f2 acc = {0.f, 0.f};
-            if (act) iters++;
-            // Position, bounds and weights; lanes that are not iterating (or fail the bounds
-            // test) run the chain loop on a safe address and drop the result, so the loop
-            // below is wave-uniform.
-            int inx = (int)floorf(nx), iny = (int)floorf(ny);
-            if (act && (inx < -kWin || inx >= L.w || iny < -kWin || iny >= L.h)) {
-                act = false;
-                if (level == 0) status = 0;
-            }
-            if (!act) { inx = 0; iny = 0; }
-            const float fa = nx - (float)inx, fb = ny - (float)iny;
-            int v00, v01, v10, v11;
-            lk_weights(fa, fb, v00, v01, v10, v11);
-            // signed: w11 = 16384 - w00 - w01 - w10 can be -1 after rounding
-            const s2 W0 = {(short)v00, (short)v01};
-            const s2 W1 = {(short)v10, (short)v11};
-            const int s = inx + k;
-            const int o = s & 3;
-            const unsigned sel = (unsigned)o | 0x0c00u | ((unsigned)(o + 1) << 16) | 0x0c000000u;
-            const uint32_t* jrow = reinterpret_cast<const uint32_t*>(Jb + (long long)iny * pitch + (s - o));
-            const int jstride = pitch >> 2;
-            uint32_t r0[12], r1[12];
-            {
-                const uint4_a4* p4 = reinterpret_cast<const uint4_a4*>(jrow);
-#pragma unroll
-                for (int t = 0; t < 3; t++) {
-                    const uint4 w = p4[t];
-                    r0[4 * t] = w.x; r0[4 * t + 1] = w.y; r0[4 * t + 2] = w.z; r0[4 * t + 3] = w.w;
-                }
-            }
-            const uint32_t* dp = r.drow;
-            const uint32_t* ip = r.irow;
-            for (int y = 0; y < kWin; y++, dp += r.dstride, ip += r.istride) {
-                jrow += jstride;
-                const uint4_a4* p4 = reinterpret_cast<const uint4_a4*>(jrow);
-#pragma unroll
-                for (int t = 0; t < 3; t++) {
-                    const uint4 w = p4[t];
-                    r1[4 * t] = w.x; r1[4 * t + 1] = w.y; r1[4 * t + 2] = w.z; r1[4 * t + 3] = w.w;
-                }
-                uint32_t d[10], iw[6], iv[5];
-                {
-                    const uint4_a4* v4 = reinterpret_cast<const uint4_a4*>(dp);
-                    const uint4 w0 = v4[0], w1 = v4[1];
-                    const uint2 w2 = *reinterpret_cast<const uint2_a4*>(dp + 8);
-                    d[0] = w0.x; d[1] = w0.y; d[2] = w0.z; d[3] = w0.w;
-                    d[4] = w1.x; d[5] = w1.y; d[6] = w1.z; d[7] = w1.w;
-                    d[8] = w2.x; d[9] = w2.y;
-                    const uint4 u0 = *reinterpret_cast<const uint4_a4*>(ip);
-                    const uint2 u1 = *reinterpret_cast<const uint2_a4*>(ip + 4);
-                    iw[0] = u0.x; iw[1] = u0.y; iw[2] = u0.z; iw[3] = u0.w; iw[4] = u1.x; iw[5] = u1.y;
-#pragma unroll
-                    for (int t = 0; t < 5; t++) iv[t] = __builtin_amdgcn_alignbit(iw[t + 1], iw[t], r.ishift);
-                }
-#pragma unroll
-                for (int g = 0; g < 10; g++) {
-                    const s2 pa = __builtin_bit_cast(s2, __builtin_amdgcn_perm(r0[g + 1], r0[g], sel));
-                    const s2 pb = __builtin_bit_cast(s2, __builtin_amdgcn_perm(r1[g + 1], r1[g], sel));
-                    const int jv = __builtin_amdgcn_sdot2(pa, W0, __builtin_amdgcn_sdot2(pb, W1, 256, false), false) >> 9;
-                    const int ival = (g & 1) ? (int)(iv[g >> 1] >> 16) : (int)(iv[g >> 1] & 0xffffu);
-                    const float fd = (float)(jv - ival);
-                    const f2 f = {(float)(int16_t)d[g], (float)((int)d[g] >> 16)};
-                    acc = acc + f * fd;
-                }
-#pragma unroll
-                for (int t = 0; t < 12; t++) r0[t] = r1[t];
-            }
-            if (!act) acc = f2{0.f, 0.f};
-            // b = (P0+P2) + (P1+P3) across the quad; inactive quads compute garbage they ignore
-            const float b1s = (quad_bcast<0>(acc.x) + quad_bcast<2>(acc.x)) + (quad_bcast<1>(acc.x) + quad_bcast<3>(acc.x));
-            const float b2s = (quad_bcast<0>(acc.y) + quad_bcast<2>(acc.y)) + (quad_bcast<1>(acc.y) + quad_bcast<3>(acc.y));
-            if (act) {
-                const float b1 = b1s * FLT_SCALE, b2 = b2s * FLT_SCALE;
-                const float dx = (A12 * b2 - A22 * b1) * Dinv;
-                const float dy = (A12 * b1 - A11 * b2) * Dinv;
-                if (a.dbg && pt == a.dbg_pt && pair == 0) {
-                    float4* t = a.dbg + (long long)a.g.nlev * a.npts + (level * 16 + j) * 4;
-                    if (k == 0) { t[0] = make_float4(b1s, b2s, dx, dy); t[1] = make_float4(nx, ny, A11, Dinv); }
-                    t[2 + (k >> 1)] = make_float4(k & 1 ? 0.f : acc.x, k & 1 ? 0.f : acc.y, acc.x, acc.y);
-                }
-                nx = nx + dx;
-                ny = ny + dy;
-                npx = nx + HALFW;
-                npy = ny + HALFW;
-                if ((double)dx * dx + (double)dy * dy <= a.eps2) {
-                    act = false;
-                } else if (j > 0 && fabs((double)fabsf(dx + pdx)) < 0.01 && fabs((double)fabsf(dy + pdy)) < 0.01) {
-                    npx = npx - dx * 0.5f;
-                    npy = npy - dy * 0.5f;
-                    act = false;
-                }
-                pdx = dx;
-                pdy = dy;
-            }
-        }
-        if (level == 0 && valid && status) {
-            const int fx = (int)floorf(npx - HALFW), fy = (int)floorf(npy - HALFW);
-            if (fx < -kWin || fx >= L.w || fy < -kWin || fy >= L.h) status = 0;
-        }
-        if (a.dbg && valid && k == 0)
-            a.dbg[((long long)pair * a.g.nlev + level) * a.npts + pt] = make_float4(npx, npy, (float)iters, (float)status);
+    const float scale = (float)(1. / (1 << level));
+    const float px0 = (float)(gx * a.pixel_step), py0 = (float)(gy * a.pixel_step);
+    const float ppx = px0 * scale - HALFW, ppy = py0 * scale - HALFW;
+    const int ipx = (int)floorf(ppx), ipy = (int)floorf(ppy);
+    bool ok = valid && !(ipx < -kWin || ipx >= L.w || ipy < -kWin || ipy >= L.h);
+
+    // group (8 points) geometry: its first slot holds its leftmost point (runs sorted by x)
+    const int slot0 = (w / a.ny) * 16 + grp * 8;
+    const int gx0v = slot0 < C.nxp ? xo[slot0] : -1;
+    const int gx0 = gx0v >= 0 ? gx0v : 0;
+    const int ipx0 = (int)floorf((float)(gx0 * a.pixel_step) * scale - HALFW);
+    const int m = (1 << level) - 1;
+    const int cx = class_of(a.cmap, level, 0, (gx0 * a.pixel_step) & m);
+    const int cy = class_of(a.cmap, level, 1, (gy * a.pixel_step) & m);
+    const uint8_t* cbase = cls + (long long)pair * a.plan.bytes_per_pair + C.off +
+                           (long long)(cy * C.nrx + cx) * C.class_bytes;
+    const int ub = min(max(ipx0 + kPad, 0), C.PW - UW);          // union start column
+    const int off = min(max(ipx + kPad - ub, 0), UW - kWin);     // this point's column in it
+    const uint32_t* gD = reinterpret_cast<const uint32_t*>(cbase) + ub + 4 * gl;
+    const uint32_t* gC = gD + (long long)C.UH * C.PW;
+    const int v0 = min(max(ipy + kPad, 0), C.UH - kWin);          // first window row (wave-uniform)
+    const uint32_t* lD0 = &lds[0][grp][0][off + k];
+    const uint32_t* lC0 = &lds[0][grp][1][off + k];
+    constexpr int LBUF = 2 * 2 * UW;                              // words per buffer
+
+    float npx, npy;
+    if (level == a.maxl) {
+        npx = px0 * scale;
+        npy = py0 * scale;
+    } else {
+        const float2 q = valid ? reinterpret_cast<const float2*>(a.next_pts)[po] : make_float2(0.f, 0.f);
+        npx = q.x * 2.f;
+        npy = q.y * 2.f;
     }
+    int status = 1;
+    if (valid && !ok && level == 0) status = 0;
+
+    uint4 rd[NCH], rc[NCH];
+    auto gload = [&](int v, bool withC) {
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const u4a4 t = *reinterpret_cast<const u4a4*>(gD + (long long)v * C.PW + 128 * c);
+            rd[c] = make_uint4(t.x, t.y, t.z, t.w);
+            if (withC) {
+                const u4a4 s = *reinterpret_cast<const u4a4*>(gC + (long long)v * C.PW + 128 * c);
+                rc[c] = make_uint4(s.x, s.y, s.z, s.w);
+            }
+        }
+    };
+    auto lstore = [&](int buf, bool withC) {
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            *reinterpret_cast<uint4*>(&lds[buf][grp][0][128 * c + 4 * gl]) = rd[c];
+            if (withC) *reinterpret_cast<uint4*>(&lds[buf][grp][1][128 * c + 4 * gl]) = rc[c];
+        }
+    };
+
+    // ---- A sums: lane k owns SSE lane k (columns 4g+k), rows in order; ((P0+P1)+P2)+P3
+    float A11, A12, A22;
+    {
+        f2 sd = {0.f, 0.f};
+        float s12 = 0.f;
+        gload(v0, false);
+        lstore(0, false);
+        __syncthreads();
+#pragma unroll 2
+        for (int y = 0; y < kWin; y++) {
+            const int buf = y & 1;
+            if (y + 1 < kWin) gload(v0 + y + 1, false);
+            const uint32_t* ld = lD0 + buf * LBUF;
+#pragma unroll
+            for (int g = 0; g < 10; g++) {
+                const uint32_t d = ld[4 * g];
+                const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
+                sd = sd + f * f;                 // (Ix*Ix, Iy*Iy)
+                s12 = s12 + f.x * f.y;           // Ix*Iy
+            }
+            if (y + 1 < kWin) lstore(buf ^ 1, false);
+            __syncthreads();
+        }
+        const float a11 = ((quad_bcast<0>(sd.x) + quad_bcast<1>(sd.x)) + quad_bcast<2>(sd.x)) + quad_bcast<3>(sd.x);
+        const float a12 = ((quad_bcast<0>(s12) + quad_bcast<1>(s12)) + quad_bcast<2>(s12)) + quad_bcast<3>(s12);
+        const float a22 = ((quad_bcast<0>(sd.y) + quad_bcast<1>(sd.y)) + quad_bcast<2>(sd.y)) + quad_bcast<3>(sd.y);
+        A11 = a11 * FLT_SCALE;
+        A12 = a12 * FLT_SCALE;
+        A22 = a22 * FLT_SCALE;
+    }
+    float Dinv = 0.f;
+    if (ok) {
+        const float D = A11 * A22 - A12 * A12;
+        const float minEig = (A22 + A11 - __builtin_sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
+                             (float)(2 * kWin * kWin);
+        if (minEig < a.min_eig || D < FLT_EPSILON) {
+            ok = false;
+            if (level == 0) status = 0;
+        } else {
+            Dinv = 1.f / D;
+        }
+    }
+
+    // ---- Newton iterations
+    const int pitch = L.pitch;
+    const uint8_t* Jb = a.pyr2 + (long long)pair * a.g.img_bytes + L.img_off + L.core();
+    float nx = npx - HALFW, ny = npy - HALFW;
+    float pdx = 0.f, pdy = 0.f;
+    bool act = ok;
+    int iters = 0;
+    for (int j = 0; j < a.max_iters; j++) {
+        if (!__any(act)) break;
+        f2 acc = {0.f, 0.f};
+        if (act) iters++;
+        // Position, bounds and weights; lanes that are not iterating (or fail the bounds
+        // test) run the row loop on a safe address and drop the result, so the loop below is
+        // wave-uniform (it also carries the group's LDS staging).
+        int inx = (int)floorf(nx), iny = (int)floorf(ny);
+        if (act && (inx < -kWin || inx >= L.w || iny < -kWin || iny >= L.h)) {
+            act = false;
+            if (level == 0) status = 0;
+        }
+        if (!act) { inx = 0; iny = 0; }
+        const float fa = nx - (float)inx, fb = ny - (float)iny;
+        int v00, v01, v10, v11;
+        lk_weights(fa, fb, v00, v01, v10, v11);
+        // signed: w11 = 16384 - w00 - w01 - w10 can be -1 after rounding
+        const s2 W0 = {(short)v00, (short)v01};
+        const s2 W1 = {(short)v10, (short)v11};
+        const int o = (inx & 3) + k;
+        const unsigned sel = (unsigned)o | 0x0c00u | ((unsigned)(o + 1) << 16) | 0x0c000000u;
+        const uint32_t* jrow = reinterpret_cast<const uint32_t*>(Jb + (long long)iny * pitch + (inx & ~3));
+        const int jstride = pitch >> 2;
+        // taps of the current window row (pa) are the previous row's lower taps (pb)
+        s2 pa[10], pb[10];
+        {
+            uint32_t rj[11];
+            load_jrow_quad(jrow, k, rj);
+#pragma unroll
+            for (int g = 0; g < 10; g++) pa[g] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[g + 1], rj[g], sel));
+        }
+        gload(v0, true);
+        lstore(0, true);
+        __syncthreads();
+#pragma unroll 2
+        for (int y = 0; y < kWin; y++) {
+            const int buf = y & 1;
+            if (y + 1 < kWin) gload(v0 + y + 1, true);
+            jrow += jstride;
+            uint32_t rj[11];
+            load_jrow_quad(jrow, k, rj);
+            const uint32_t* ld = lD0 + buf * LBUF;
+            const uint32_t* lc = lC0 + buf * LBUF;
+#pragma unroll
+            for (int g = 0; g < 10; g++) {
+                pb[g] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[g + 1], rj[g], sel));
+                // (J*32 - I*32) exactly as the reference's CV_DESCALE(...) - I
+                const int jd = __builtin_amdgcn_sdot2(pa[g], W0, __builtin_amdgcn_sdot2(pb[g], W1, (int)lc[4 * g], false),
+                                                      false) >> 9;
+                const float fd = (float)jd;
+                const uint32_t d = ld[4 * g];
+                const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
+                acc = acc + f * fd;
+                pa[g] = pb[g];
+            }
+            if (y + 1 < kWin) lstore(buf ^ 1, true);
+            __syncthreads();
+        }
+        if (!act) acc = f2{0.f, 0.f};
+        // b = (P0+P2) + (P1+P3) across the quad; inactive quads compute garbage they ignore
+        const float b1s = (quad_bcast<0>(acc.x) + quad_bcast<2>(acc.x)) + (quad_bcast<1>(acc.x) + quad_bcast<3>(acc.x));
+        const float b2s = (quad_bcast<0>(acc.y) + quad_bcast<2>(acc.y)) + (quad_bcast<1>(acc.y) + quad_bcast<3>(acc.y));
+        if (act) {
+            const float b1 = b1s * FLT_SCALE, b2 = b2s * FLT_SCALE;
+            const float dx = (A12 * b2 - A22 * b1) * Dinv;
+            const float dy = (A12 * b1 - A11 * b2) * Dinv;
+            if (a.dbg && pt == a.dbg_pt && pair == 0) {
+                float4* t = a.dbg + (long long)a.g.nlev * a.npts + (level * 16 + j) * 4;
+                if (k == 0) { t[0] = make_float4(b1s, b2s, dx, dy); t[1] = make_float4(nx, ny, A11, Dinv); }
+                t[2 + (k >> 1)] = make_float4(k & 1 ? 0.f : acc.x, k & 1 ? 0.f : acc.y, acc.x, acc.y);
+            }
+            nx = nx + dx;
+            ny = ny + dy;
+            npx = nx + HALFW;
+            npy = ny + HALFW;
+#ifdef LKX_FIXED   // timing-only builds (scripts/lk_variants.sh): a fixed iteration count
+            if (j + 1 >= LKX_FIXED) act = false;
+#else
+            if ((double)dx * dx + (double)dy * dy <= a.eps2) {
+                act = false;
+            } else if (j > 0 && fabs((double)fabsf(dx + pdx)) < 0.01 && fabs((double)fabsf(dy + pdy)) < 0.01) {
+                npx = npx - dx * 0.5f;
+                npy = npy - dy * 0.5f;
+                act = false;
+            }
+#endif
+            pdx = dx;
+            pdy = dy;
+        }
+    }
+    if (level == 0 && valid && status) {
+        const int fx = (int)floorf(npx - HALFW), fy = (int)floorf(npy - HALFW);
+        if (fx < -kWin || fx >= L.w || fy < -kWin || fy >= L.h) status = 0;
+    }
+    if (a.dbg && valid && k == 0)
+        a.dbg[((long long)pair * a.g.nlev + level) * a.npts + pt] = make_float4(npx, npy, (float)iters, (float)status);
     if (valid && k == 0) {
-        const long long o = (long long)pair * a.npts + pt;
-        a.next_pts[2 * o] = npx;
-        a.next_pts[2 * o + 1] = npy;
-        a.status[o] = (uint8_t)status;
+        reinterpret_cast<float2*>(a.next_pts)[po] = make_float2(npx, npy);
+        if (level == 0) a.status[po] = (uint8_t)status;
     }
 }
 
-hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint8_t* cls, float4* Abuf)
+hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint8_t* cls)
 {
-    for (int l = 0; l <= a.maxl; l++) {
+    for (int l = a.maxl; l >= 0; l--) {
+        // class planes of this level right before its use: they are still in L2 / MALL
         const ClassLevel& C = a.plan.lv[l];
         LkClassArgs ca;
         ca.g = a.g;
         ca.plan = a.plan;
         ca.rlist = a.rlist;
         ca.level = l;
-        const dim3 grid((C.PW + 63) / 64, C.UH, batch * C.nrx * C.nry);
+        const dim3 grid((C.PW / 4 + 63) / 64, C.UH, batch * C.nrx * C.nry);
         hipLaunchKernelGGL(k_lk_class, grid, dim3(64), 0, s, a.pyr1, a.der, cls, ca);
+        const dim3 lg(((C.nxp + 15) / 16) * a.ny, batch);
+        switch (a.plan.nch) {
+        case 1: hipLaunchKernelGGL(k_lk_level<1>, lg, dim3(64), 0, s, a, cls, l); break;
+        case 2: hipLaunchKernelGGL(k_lk_level<2>, lg, dim3(64), 0, s, a, cls, l); break;
+        case 4: hipLaunchKernelGGL(k_lk_level<4>, lg, dim3(64), 0, s, a, cls, l); break;
+        default: return hipErrorInvalidValue;
+        }
     }
-    const int nx = (a.npts + a.ny - 1) / a.ny;
-    const int nwaves = ((nx + 15) / 16) * a.ny;
-    hipLaunchKernelGGL(k_lk_A, dim3(nwaves, a.maxl + 1, batch), dim3(64), 0, s, a, cls, Abuf);
-    hipLaunchKernelGGL(k_lk_track, dim3(nwaves, batch), dim3(64), 0, s, a, cls, Abuf);
     return hipGetLastError();
 }
 
