@@ -79,6 +79,13 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+def throughput(D: Dist, units_local: float, seconds_local: float):
+    """Whole-job rate: units processed by all ranks / max-over-ranks wall time (the slowest
+    shard bounds the job).  Returns (rate, max_seconds)."""
+    t = D.max(seconds_local)
+    return D.sum(units_local) / t, t
+
+
 def make_batch(w: int, h: int, batch: int, unique: int, seed0: int, threads: int):
     """`unique` distinct synthetic pairs replicated to `batch` slots (distinct HBM addresses,
     so the working set still exceeds the 256 MB Infinity Cache)."""
@@ -162,12 +169,12 @@ def main():
     ctx.device_sync()
     D.barrier()
     el = time.perf_counter() - t0
-    el_max = D.max(el)
+    px_rate, el_max = throughput(D, float(args.steps * B * w * h), el)
+    value = px_rate / 1e6
+    px_all = px_rate * el_max
     st = ctx.stage_ms()
     calls = max(st["calls"], 1)
     stages = {k: round(v / calls, 4) for k, v in st.items() if k != "calls"}
-    px_all = D.sum(float(args.steps * B * w * h))
-    value = px_all / 1e6 / el_max
     for p in (d1, d2, dmask, dnum):
         ctx.dev_free(p)
     del g1, g2
