@@ -10,7 +10,7 @@
 //   A3      k_scharr         calcSharrDeriv + CONSTANT-0 padding (prev frame)
 //   A5      k_lk             calcOpticalFlowPyrLK (LKTrackerInvoker, SSE2 summation order)
 //   A6/A7   k_classify_fit   Vec4d classification, first-4 getPerspectiveTransform, invert
-//   A8-A10  k_warp_diff      warpPerspective + absdiff + threshold, fused
+//   A8-A10  k_warp_diff      warpPerspective + absdiff + threshold, fused (mdx_warp.hip)
 #include "mdx_internal.h"
 
 #include <float.h>
@@ -639,105 +639,7 @@ __global__ void k_export_fit(const PairFit* __restrict__ fits, int batch, double
     if (num) num[pair] = fits[pair].num_vectors;
 }
 
-// ------------------------------------------------------------------ A8-A10: warp + diff
-// warpPerspective(gray1, M) with M^-1 precomputed (fit.Hinv): imgwarp.cpp
-// warpPerspectiveInvoker, BLOCK_SZ 32 -> blocks of bw0 x bh0 (64 x 16 for W>=64, H>=16);
-// per pixel X = cvRound(clamp((X0 + M0*x1) * (W ? 32/W : 0))), W = W0 + M6*x1 with
-// X0 = M0*xb + M1*y + M2 at the block's left column xb; then remapBilinear with the 32x32
-// fixed-point table (weights (32-fx)(32-fy)*32 ..., +16384 >> 15) and BORDER_CONSTANT 0,
-// fused with absdiff and threshold: mask = |warp - gray2| > thresh ? 255 : 0.
-// A workgroup covers one 64 x 16 tile (the reference's block), 4 pixels per thread.
-__device__ __forceinline__ int clamp_int_from_double(double v)
-{
-    // std::max((double)INT_MIN, std::min((double)INT_MAX, v)) then cvRound
-    double r = (v < (double)INT_MAX) ? v : (double)INT_MAX;
-    r = ((double)INT_MIN < r) ? r : (double)INT_MIN;
-    return (int)__builtin_rint(r);
-}
-
-template <bool AFFINE>
-__device__ __forceinline__ void warp_coord(const double* M, double X0, double Y0, double W0, double Wc, int x1,
-                                           int& X, int& Y)
-{
-    double Wd;
-    if (AFFINE) {
-        Wd = Wc;
-    } else {
-        const double Wv = W0 + M[6] * x1;
-        Wd = Wv != 0.0 ? 32.0 / Wv : 0.0;
-    }
-    const double fX = (X0 + M[0] * x1) * Wd;
-    const double fY = (Y0 + M[3] * x1) * Wd;
-    X = clamp_int_from_double(fX);
-    Y = clamp_int_from_double(fY);
-}
-
-__global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
-                                                   const uint8_t* __restrict__ g2, long long g2_stride, int g2_pitch,
-                                                   int w, int h, int bw0, const PairFit* __restrict__ fits,
-                                                   uint8_t* __restrict__ mask, long long mask_stride, int thresh)
-{
-    const int pair = blockIdx.z;
-    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-    const int y = blockIdx.y * 16 + ty;
-    const int x0 = blockIdx.x * 64 + tx * 4;
-    if (y >= h || x0 >= w) return;
-    const PairFit& f = fits[pair];
-    uint8_t* mrow = mask + (long long)pair * mask_stride + (long long)y * w;
-    const int n = min(4, w - x0);
-    if (f.fit_status != 0) {
-        for (int k = 0; k < n; k++) mrow[x0 + k] = 0;
-        return;
-    }
-    double M[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) M[k] = f.Hinv[k];
-    const bool affine = (M[6] == 0.0) && (M[7] == 0.0);
-    const double Wc = M[8] != 0.0 ? 32.0 / M[8] : 0.0;
-    const uint8_t* src = g1 + (long long)pair * g1_stride;
-    const uint8_t* r2 = g2 + (long long)pair * g2_stride + (long long)y * g2_pitch;
-    uint8_t out[4] = {0, 0, 0, 0};
-    int xb_prev = -1;
-    double X0 = 0, Y0 = 0, W0 = 0;
-    for (int k = 0; k < n; k++) {
-        const int x = x0 + k;
-        const int xb = (x / bw0) * bw0, x1 = x - xb;
-        if (xb != xb_prev) {
-            X0 = M[0] * xb + M[1] * y + M[2];
-            Y0 = M[3] * xb + M[4] * y + M[5];
-            W0 = M[6] * xb + M[7] * y + M[8];
-            xb_prev = xb;
-        }
-        int X, Y;
-        if (affine) warp_coord<true>(M, X0, Y0, W0, Wc, x1, X, Y);
-        else warp_coord<false>(M, X0, Y0, W0, Wc, x1, X, Y);
-        const int sx = min(max(X >> 5, -32768), 32767), sy = min(max(Y >> 5, -32768), 32767);
-        const int fx = X & 31, fy = Y & 31;
-        // (0,0) cell of BilinearTab_i is {32767,0,0,1}; for 8-bit data it yields the same
-        // value as {32768,0,0,0}, which is what the plain formula below computes.
-        const int wt0 = (32 - fx) * (32 - fy) * 32, wt1 = fx * (32 - fy) * 32;
-        const int wt2 = (32 - fx) * fy * 32, wt3 = fx * fy * 32;
-        const bool ix0 = (unsigned)sx < (unsigned)w, ix1 = (unsigned)(sx + 1) < (unsigned)w;
-        const bool iy0 = (unsigned)sy < (unsigned)h, iy1 = (unsigned)(sy + 1) < (unsigned)h;
-        const int cx0 = min(max(sx, 0), w - 1), cx1 = min(max(sx + 1, 0), w - 1);
-        const int cy0 = min(max(sy, 0), h - 1), cy1 = min(max(sy + 1, 0), h - 1);
-        const uint8_t* ra = src + (long long)cy0 * g1_pitch;
-        const uint8_t* rb = src + (long long)cy1 * g1_pitch;
-        const int v0 = (ix0 && iy0) ? ra[cx0] : 0;
-        const int v1 = (ix1 && iy0) ? ra[cx1] : 0;
-        const int v2 = (ix0 && iy1) ? rb[cx0] : 0;
-        const int v3 = (ix1 && iy1) ? rb[cx1] : 0;
-        int v = (v0 * wt0 + v1 * wt1 + v2 * wt2 + v3 * wt3 + (1 << 14)) >> 15;
-        v = min(max(v, 0), 255);
-        const int d = abs(v - (int)r2[x]);
-        out[k] = d > thresh ? 255 : 0;
-    }
-    if (n == 4 && ((((uintptr_t)(mrow + x0)) & 3) == 0)) {
-        *reinterpret_cast<uchar4*>(mrow + x0) = make_uchar4(out[0], out[1], out[2], out[3]);
-    } else {
-        for (int k = 0; k < n; k++) mrow[x0 + k] = out[k];
-    }
-}
+// A8-A10 (warp + absdiff + threshold) lives in mdx_warp.hip.
 
 // ------------------------------------------------------------------ launchers
 static inline dim3 padded_grid(int w, int h, int z, dim3 blk)
@@ -797,18 +699,6 @@ hipError_t launch_set_fit_external(hipStream_t s, int batch, const double* H_ext
 hipError_t launch_export_fit(hipStream_t s, int batch, const PairFit* fits, double* H, int* num)
 {
     hipLaunchKernelGGL(k_export_fit, dim3((batch + 63) / 64), dim3(64), 0, s, fits, batch, H, num);
-    return hipGetLastError();
-}
-
-hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,
-                            const uint8_t* g2, long long g2_stride, int g2_pitch, int w, int h, const PairFit* fits,
-                            uint8_t* mask, long long mask_stride, int thresh)
-{
-    const int bh0 = h < 16 ? h : 16;
-    const int bw0 = (1024 / bh0) < w ? (1024 / bh0) : w;
-    const dim3 grid((w + 63) / 64, (h + 15) / 16, batch);
-    hipLaunchKernelGGL(k_warp_diff, grid, dim3(256), 0, s, g1, g1_stride, g1_pitch, g2, g2_stride, g2_pitch, w, h, bw0,
-                       fits, mask, mask_stride, thresh);
     return hipGetLastError();
 }
 
