@@ -128,6 +128,7 @@ def main():
     ap.add_argument("--roofline-config", default="4k", choices=sorted(CONFIGS))
     ap.add_argument("--roofline-batch", type=int, default=32)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--only-roofline", action="store_true", help="profiling aid: only the warp+diff roofline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_warp_diff.json"),
@@ -143,7 +144,10 @@ def main():
     unique = max(1, min(args.unique, B))
     ps = 10
 
-    g1, g2, Ht, uniq = make_batch(w, h, B, unique, SEED0 + 1000 * D.rank, threads)
+    g1, g2, Ht, uniq = make_batch(w, h, B if not args.only_roofline else 1, unique if not args.only_roofline else 1,
+                                  SEED0 + 1000 * D.rank, threads)
+    if args.only_roofline:
+        B, unique = 1, 1
     ctx = mdx.Context(D.local_rank, w, h, B, pixel_step=ps, min_vector_size=1.0)
     d1, d2 = ctx.dev_alloc(g1.nbytes), ctx.dev_alloc(g2.nbytes)
     dmask = ctx.dev_alloc(B * w * h)
@@ -154,7 +158,8 @@ def main():
     def step():
         ctx.flow_warp_diff_batch_dev(B, d1, d2, w, h, w, w * h, mdx.FMT_GRAY8, d_mask=dmask, d_num_vectors=dnum)
 
-    for _ in range(args.warmup):
+    full_steps = 1 if args.only_roofline else args.steps
+    for _ in range(0 if args.only_roofline else args.warmup):
         step()
     ctx.device_sync()
     num = np.empty(B, np.int32)
@@ -164,12 +169,12 @@ def main():
     D.barrier()
     ctx.device_sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(full_steps):
         step()
     ctx.device_sync()
     D.barrier()
     el = time.perf_counter() - t0
-    px_rate, el_max = throughput(D, float(args.steps * B * w * h), el)
+    px_rate, el_max = throughput(D, float(full_steps * B * w * h), el)
     value = px_rate / 1e6
     px_all = px_rate * el_max
     st = ctx.stage_ms()
@@ -229,7 +234,7 @@ def main():
         "n_gpus": D.world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(el_max / args.steps * 1e3, 3),
+        "ms_per_step": round(el_max / full_steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -11,24 +11,25 @@
 //   sx = X >> 5, fx = X & 31, ...;  out = (sum v_i * w_i + 2^14) >> 15 with w_i from (fx, fy)
 //   mask = |out - gray2| > thresh ? 255 : 0
 //
-// Fast path (affine M, bw0 == 64, the tile's source footprint small): one 256-thread workgroup
-// per 64 x 64 destination tile (= one reference block column, four block rows).  Lane l of
-// wave w owns the 4 columns x0 + 4*(l & 15) .. +3 of rows y0 + 16w + 4i + (l >> 4), i = 0..3,
-// so gray2 loads / mask stores are dwords, 64 contiguous bytes per row.
+// Fast path (affine M, bw0 == 64, full-width tile over dword-aligned buffers, the tile's source
+// footprint small): one 256-thread workgroup per 64 x 128 destination tile (= one reference block
+// column, eight block rows).  Lane l of wave w owns the 4 columns x0 + 4*(l & 15) .. +3 of rows
+// y0 + 32w + 4i + (l >> 4), i = 0..7, so gray2 loads / mask stores are dwords, 64 contiguous bytes
+// per row.  Wave 0 computes the footprint; the workgroup stages it.
 //   * The tile's source footprint (exact: X, Y are monotone in x and y for affine M, so the
 //     four corners bound it) is staged once into LDS as raw bytes with ds_write_b128, zero
-//     outside the image (= BORDER_CONSTANT 0 per tap).  Row pitch 192 B (48 dwords = 16 mod 32):
-//     the two rows a half-wave touches fall in disjoint banks; taps are 4 ds_read_u8 with
-//     immediate offsets (0, 1, 192, 193).
+//     outside the image (= BORDER_CONSTANT 0 per tap), row pitch kSP = 96 B; taps are 4 byte
+//     reads with immediate offsets (0, 1, 96, 97).
 //   * Per column, M0*x1 and M3*x1 stay in registers (4 columns per lane); per row, X0 and Y0 come
-//     from a 64-entry LDS table.  Per pixel: two FP64 adds and two multiply-adds with the magic
+//     from a 128-entry LDS table.  Per pixel: two FP64 adds and two multiply-adds with the magic
 //     constant 1.5*2^52 - 32*origin, whose low word is cvRound(.) relative to the staged origin
 //     (round-half-even, exact for |X| < 2^30, checked per tile).  When 32/M8 is a power of two the
 //     multiply is exact and fuses with the rounding add into one FMA.
-//   * Bilinear: w = (32-fx)(32-fy)*32 ... factorises exactly: h0 = dot4(v00 v01 v10 v11, 32-fx fx 0 0),
-//     h1 = dot4(., 0 0 32-fx fx), out = (dot2(h0 h1, 32-fy fy) + 512) >> 10.
-//   * |out - g2| + (255 - thresh) has bit 8 set iff the pixel is moving (v_sad_u16); four such
-//     bits are packed with v_perm and scaled by 255 into the mask dword.
+//   * Bilinear: w = (32-fx)(32-fy)*32 ... factorises exactly into three v_dot2_u32_u16 on taps
+//     loaded straight into u16 halves (ds_read_u8_d16/_hi): q0 = dot(v00 v10, 32-fy fy),
+//     q1 = dot(v01 v11, .), out = (dot(q0 q1, 32-fx fx) + 512) >> 10.
+//   * |out - g2| + (32767 - thresh) has bit 15 set iff the pixel is moving (v_sad_u16); v_perm's
+//     sign-replicating selectors turn four such bits into the four 0x00/0xff mask bytes.
 // Everything else (perspective M, small frames, huge or far-away footprints) takes the general
 // per-pixel path, exact for any input.
 #include "mdx_internal.h"
@@ -41,9 +42,18 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 
 constexpr int kWTile = 64;              // tile = one reference block column (bw0 = 64)
-constexpr int kHTile = 64;              // four reference block rows
-constexpr int kSP = 192;                // staged row pitch, bytes (48 dwords = 16 mod 32)
-constexpr int kSH = 96;                 // staged rows
+#ifndef WX_TH
+#define WX_TH 128
+#endif
+constexpr int kHTile = WX_TH;           // 16 * reference block rows (default 8 block rows)
+#ifndef WX_SP
+#define WX_SP 96
+#endif
+// staged row pitch, bytes.  96 (24 dwords) leaves some 2-way bank conflicts between the two tap
+// rows a half-wave reads, but 15 KiB of LDS per workgroup lets 8 workgroups share a CU, which
+// hides the staging latency better than the conflict-free 192 (measured 258 vs 284 us, 4K x32).
+constexpr int kSP = WX_SP;
+constexpr int kSH = 136;                // staged rows (tile height + rotation/scale margin)
 
 __device__ __forceinline__ int clamp_int_from_double(double v)
 {
@@ -129,122 +139,35 @@ __device__ TileInfo tile_info(const double* M, double Wd, int x0, int y0, int w,
     return t;
 }
 
-// grid: x -> tile column, y -> tile row, z -> pair.  256 threads.
-__global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
-                                                   const uint8_t* __restrict__ g2, long long g2_stride, int g2_pitch,
-                                                   int w, int h, int bw0, const PairFit* __restrict__ fits,
-                                                   uint8_t* __restrict__ mask, long long mask_stride, int thresh,
-                                                   int vec_ok)
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+// LDS pointers stay 32-bit (address space 3) through the inlined helper
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const d2v lds_d2;
+
+// Fast-path rows of one lane: 4 columns x nrows rows (every 4th tile row from r0).  The tile is
+// full width and the buffers dword-aligned (checked by the caller), so loads/stores are dwords.
+template <bool POW2>
+__device__ __forceinline__ void warp_rows(lds_d2* s_xy, lds_u8* s_src, int r0, int nrows, int y0, int xs,
+                                          const uint8_t* g2p, int g2_pitch, uint8_t* mp, int w, const double* tx,
+                                          const double* ty, double Wd, double mX, double mY, uint32_t bias)
 {
-    __shared__ __attribute__((aligned(16))) double s_xy[kHTile][2];    // (X0, Y0) per tile row
-    __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
-
-    const int pair = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int x0 = blockIdx.x * kWTile, y0 = blockIdx.y * kHTile;
-    const int cq = lane & 15, rr = lane >> 4;
-    const int xs = x0 + 4 * cq;                     // this lane's 4 columns
-    const int nx = max(0, min(4, w - xs));
-    const uint8_t* g2p = g2 + (long long)pair * g2_stride;
-    uint8_t* mp = mask + (long long)pair * mask_stride;
-    const bool vec = vec_ok && nx == 4;
-
-    const PairFit& f = fits[pair];
-    if (f.fit_status != 0) {   // no fit: the reference produces no mask; ours is all zero
-        for (int i = 0; i < 4; i++) {
-            const int y = y0 + 16 * wave + 4 * i + rr;
-            if (y >= h) break;
-            uint8_t* m = mp + (long long)y * w + xs;
-            if (vec) *reinterpret_cast<uint32_t*>(m) = 0u;
-            else for (int k = 0; k < nx; k++) m[k] = 0;
-        }
-        return;
-    }
-    double M[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) M[k] = f.Hinv[k];
-    const uint8_t* src = g1 + (long long)pair * g1_stride;
-    const bool affine = (M[6] == 0.0) && (M[7] == 0.0);
-    const double Wd = M[8] != 0.0 ? 32.0 / M[8] : 0.0;   // affine: W = M8 everywhere
-
-    TileInfo t;
-    t.fast = 0;
-    if (affine && bw0 == kWTile) t = tile_info(M, Wd, x0, y0, w, h, lane);
-    if (!t.fast) {
-        // ---- general path: per pixel, global gathers
-        for (int i = 0; i < 4; i++) {
-            const int y = y0 + 16 * wave + 4 * i + rr;
-            if (y >= h) break;
-            const uint8_t* g2r = g2p + (long long)y * g2_pitch + xs;
-            uint8_t* m = mp + (long long)y * w + xs;
-            for (int k = 0; k < nx; k++) m[k] = warp_px_general(M, src, g1_pitch, w, h, xs + k, y, bw0, g2r[k], thresh);
-        }
-        return;
-    }
-
-    // ---- fast path: stage the footprint, rows sya.., columns sxa.. (16-B chunks)
-    if (tid < kHTile) {
-        const int y = y0 + tid;
-        s_xy[tid][0] = M[0] * x0 + M[1] * y + M[2];
-        s_xy[tid][1] = M[3] * x0 + M[4] * y + M[5];
-    }
-    {
-        const int nch = (t.sw + 15) >> 4;
-        for (int e = tid; e < nch * t.sh; e += 256) {
-            const int r = e / nch, ch = e - r * nch;
-            const int sy = t.sya + r, sx = t.sxa + 16 * ch;
-            uint4 v;
-            if ((unsigned)sy < (unsigned)h && sx >= 0 && sx + 16 <= w) {
-                const uint8_t* p = src + (long long)sy * g1_pitch + sx;
-                v = *reinterpret_cast<const uint4*>(p);
-            } else {
-                uint32_t d[4] = {0, 0, 0, 0};
-                if ((unsigned)sy < (unsigned)h) {
-                    const uint8_t* p = src + (long long)sy * g1_pitch;
-                    for (int i = 0; i < 16; i++) {
-                        const int xx = sx + i;
-                        if ((unsigned)xx < (unsigned)w) d[i >> 2] |= (uint32_t)p[xx] << (8 * (i & 3));
-                    }
-                }
-                v = make_uint4(d[0], d[1], d[2], d[3]);
-            }
-            *reinterpret_cast<uint4*>(&s_src[r * kSP + 16 * ch]) = v;
-        }
-    }
-    __syncthreads();
-    if (nx == 0) return;
-
-    const double magic = 6755399441055744.0;                 // 1.5 * 2^52
-    const double mX = magic - 32.0 * t.sxa, mY = magic - 32.0 * t.sya;
-    // 32/M8 a power of two -> (X0 + M0*x1) * Wd is exact and fuses with the rounding add
-    const bool pow2 = Wd != 0.0 && (__double_as_longlong(Wd) & 0x000fffffffffffffLL) == 0;
-    const uint32_t bias = 255u - (uint32_t)thresh;
-    double tx[4], ty[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        tx[k] = M[0] * (4 * cq + k);
-        ty[k] = M[3] * (4 * cq + k);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int r = 16 * wave + 4 * i + rr;
-        const int y = y0 + r;
-        if (y >= h) break;
-        const double2 xy = *reinterpret_cast<const double2*>(s_xy[r]);
-        const uint8_t* g2r = g2p + (long long)y * g2_pitch + xs;
-        uint32_t G;
-        if (vec) {
-            G = *reinterpret_cast<const uint32_t*>(g2r);
-        } else {
-            G = 0;
-            for (int k = 0; k < nx; k++) G |= (uint32_t)g2r[k] << (8 * k);
-        }
-        uint32_t e4[4];
+    const uint8_t* g2r = g2p + (long long)(y0 + r0) * g2_pitch + xs;
+    uint8_t* mr = mp + (long long)(y0 + r0) * w + xs;
+    const long long g2s = 4LL * g2_pitch, ms = 4LL * w;
+    for (int i = 0; i < nrows; i++, g2r += g2s, mr += ms) {
+        const d2v xy = s_xy[r0 + 4 * i];
+#ifndef WX_NO_G2   // WX_*: timing-only builds (scripts/warp_variants.sh), results invalid
+        const uint32_t G = *reinterpret_cast<const uint32_t*>(g2r);
+#else
+        const uint32_t G = (uint32_t)i * 0x01010101u;
+#endif
+        uint32_t wxs[4], wys[4], c0s[4], c1s[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const double ax = xy.x + tx[k], ay = xy.y + ty[k];
             double rx, ry;
-            if (pow2) {
+            if (POW2) {
                 rx = __builtin_fma(ax, Wd, mX);
                 ry = __builtin_fma(ay, Wd, mY);
             } else {
@@ -254,27 +177,179 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
             const uint32_t X = (uint32_t)__double2loint(rx);   // cvRound((...)*Wd) - 32*sxa, >= 0
             const uint32_t Y = (uint32_t)__double2loint(ry);
             const uint32_t fx = X & 31u, fy = Y & 31u;
-            const uint8_t* tp = s_src + (Y >> 5) * kSP + (X >> 5);
-            const uint32_t v00 = tp[0], v01 = tp[1], v10 = tp[kSP], v11 = tp[kSP + 1];
-            const uint32_t P = v00 | (v01 << 8) | (v10 << 16) | (v11 << 24);
-            const uint32_t wxb = fx * 255u + 32u;                 // bytes (32 - fx, fx)
-            const uint32_t h0 = __builtin_amdgcn_udot4(P, wxb, 0u, false);
-            const uint32_t h1 = __builtin_amdgcn_udot4(P, wxb << 16, 0u, false);
-            const uint32_t wy = fy * 65535u + 32u;                // u16 (32 - fy, fy)
-            const uint32_t sv = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, h0 | (h1 << 16)),
-                                                       __builtin_bit_cast(u16x2, wy), 512u, false);
-            const uint32_t v = sv >> 10;
-            e4[k] = __builtin_amdgcn_sad_u16(v, (G >> (8 * k)) & 255u, bias);   // |v - g| + bias: bit 8 iff > thresh
+            const uint32_t off = __umul24(Y >> 5, (uint32_t)kSP) + (X >> 5);   // v_mad_u32_u24
+            wxs[k] = fx * 65535u + 32u;                 // u16 (32 - fx, fx)
+            wys[k] = fy * 65535u + 32u;                 // u16 (32 - fy, fy)
+#ifndef WX_NO_TAPS
+#ifdef WX_D16
+            // taps straight into u16 halves: c0 = (v00, v10), c1 = (v01, v11)
+            const uint32_t a = (uint32_t)(uintptr_t)(s_src + off);
+            uint32_t c0, c1;
+            asm volatile("ds_read_u8_d16 %0, %2\n\t"
+                         "ds_read_u8_d16_hi %0, %2 offset:%3\n\t"
+                         "ds_read_u8_d16 %1, %2 offset:1\n\t"
+                         "ds_read_u8_d16_hi %1, %2 offset:%4"
+                         : "=&v"(c0), "=&v"(c1) : "v"(a), "i"(kSP), "i"(kSP + 1));
+            c0s[k] = c0;
+            c1s[k] = c1;
+#else
+            c0s[k] = (uint32_t)s_src[off] | ((uint32_t)s_src[off + kSP] << 16);
+            c1s[k] = (uint32_t)s_src[off + 1] | ((uint32_t)s_src[off + kSP + 1] << 16);
+#endif
+#else
+            c0s[k] = (off & 255) | (((off >> 3) & 255) << 16);
+            c1s[k] = ((off >> 5) & 255) | (((off >> 7) & 255) << 16);
+#endif
         }
-        // byte 1 of each e4[k] is 0 or 1 -> pack, scale by 255
-        const uint32_t p01 = __builtin_amdgcn_perm(e4[1], e4[0], 0x0c0c0501u);
-        const uint32_t p23 = __builtin_amdgcn_perm(e4[3], e4[2], 0x0c0c0501u);
-        const uint32_t b = p01 | (p23 << 16);
-        const uint32_t out = (b << 8) - b;
-        uint8_t* m = mp + (long long)y * w + xs;
-        if (vec) *reinterpret_cast<uint32_t*>(m) = out;
-        else for (int k = 0; k < nx; k++) m[k] = (uint8_t)(out >> (8 * k));
+#if defined(WX_D16) && !defined(WX_NO_TAPS)
+        // the asm loads are invisible to the compiler's waitcnt pass: wait here, and make every
+        // tap register an operand so no use can be scheduled above the wait
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(c0s[0]), "+v"(c0s[1]), "+v"(c0s[2]), "+v"(c0s[3]), "+v"(c1s[0]), "+v"(c1s[1]),
+                       "+v"(c1s[2]), "+v"(c1s[3])
+                     :
+                     : "memory");
+#endif
+        uint32_t e4[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            // vertical then horizontal: sum_i v_i (32-fx|fx)(32-fy|fy), exact in integers
+            const uint32_t q0 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, c0s[k]), __builtin_bit_cast(u16x2v, wys[k]), 0u, false);
+            const uint32_t q1 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, c1s[k]), __builtin_bit_cast(u16x2v, wys[k]), 0u, false);
+            const uint32_t sv = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, q0 | (q1 << 16)),
+                                                       __builtin_bit_cast(u16x2v, wxs[k]), 512u, false);
+            const uint32_t v = sv >> 10;
+            // |v - g| + 32767 - thresh: bit 15 set iff |v - g| > thresh (value < 2^16)
+            e4[k] = __builtin_amdgcn_sad_u16(v, (G >> (8 * k)) & 255u, bias);
+        }
+        // v_perm selectors 8 / 10 replicate bit 15 / bit 47 of {src0:src1}: 0xff or 0x00 bytes
+        const uint32_t e01 = e4[0] | (e4[1] << 16), e23 = e4[2] | (e4[3] << 16);
+        const uint32_t out = __builtin_amdgcn_perm(e23, e01, 0x0b0a0908u);
+#ifndef WX_NO_STORE
+        *reinterpret_cast<uint32_t*>(mr) = out;
+#else
+        if (out == bias) *reinterpret_cast<uint32_t*>(mr) = out;   // runtime-false: keeps the work
+#endif
     }
+}
+
+// grid: x -> tile column, y -> tile row, z -> pair.  256 threads; lane l of wave q owns columns
+// x0 + 4*(l & 15) .. +3 of tile rows 32q + (l >> 4) + 4i, i = 0..7.
+__global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
+                                                   const uint8_t* __restrict__ g2, long long g2_stride, int g2_pitch,
+                                                   int w, int h, int bw0, const PairFit* __restrict__ fits,
+                                                   uint8_t* __restrict__ mask, long long mask_stride, int thresh,
+                                                   int vec_ok)
+{
+    __shared__ __attribute__((aligned(16))) double s_xy[kHTile][2];    // (X0, Y0) per tile row
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
+    __shared__ TileInfo s_info;
+
+    const int pair = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int x0 = blockIdx.x * kWTile, y0 = blockIdx.y * kHTile;
+    const int cq = lane & 15, rr = lane >> 4;
+    const int xs = x0 + 4 * cq;                     // this lane's 4 columns
+    const int r0 = (kHTile / 4) * wave + rr;        // this lane's first tile row
+    const int nrows = max(0, min(kHTile / 16, (h - y0 - r0 + 3) >> 2));
+    const uint8_t* g2p = g2 + (long long)pair * g2_stride;
+    uint8_t* mp = mask + (long long)pair * mask_stride;
+
+    const PairFit& f = fits[pair];
+    if (f.fit_status != 0) {   // no fit: the reference produces no mask; ours is all zero
+        const int nx = max(0, min(4, w - xs));
+        for (int i = 0; i < nrows; i++) {
+            uint8_t* m = mp + (long long)(y0 + r0 + 4 * i) * w + xs;
+            for (int k = 0; k < nx; k++) m[k] = 0;
+        }
+        return;
+    }
+    double M[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) M[k] = f.Hinv[k];
+    const uint8_t* src = g1 + (long long)pair * g1_stride;
+    const bool affine = (M[6] == 0.0) && (M[7] == 0.0);
+    const double Wd = M[8] != 0.0 ? 32.0 / M[8] : 0.0;   // affine: W = M8 everywhere
+    // fast path only for full-width tiles over dword-aligned rows (uniform per workgroup)
+    const bool try_fast = affine && bw0 == kWTile && vec_ok && x0 + kWTile <= w;
+
+    if (try_fast && wave == 0) {
+        const TileInfo t = tile_info(M, Wd, x0, y0, w, h, lane);
+        if (lane == 0) s_info = t;
+    }
+    if (try_fast) __syncthreads();
+    const TileInfo t = s_info;
+    if (!try_fast || !t.fast) {
+        // ---- general path: per pixel, global gathers
+        const int nx = max(0, min(4, w - xs));
+        for (int i = 0; i < nrows; i++) {
+            const int y = y0 + r0 + 4 * i;
+            const uint8_t* g2r = g2p + (long long)y * g2_pitch + xs;
+            uint8_t* m = mp + (long long)y * w + xs;
+            for (int k = 0; k < nx; k++) m[k] = warp_px_general(M, src, g1_pitch, w, h, xs + k, y, bw0, g2r[k], thresh);
+        }
+        return;
+    }
+
+    // ---- fast path: per-row X0/Y0, then stage the footprint (rows sya.., 16-B chunks from sxa)
+    if (tid < kHTile) {
+        const int y = y0 + tid;
+        s_xy[tid][0] = M[0] * x0 + M[1] * y + M[2];
+        s_xy[tid][1] = M[3] * x0 + M[4] * y + M[5];
+    }
+    {
+        const int nch = (t.sw + 15) >> 4;                 // <= kSP / 16
+        const int rpp = 256 / nch;                        // rows per pass
+        const int ro = tid / nch, ch = tid - ro * nch;    // once per thread
+        const int sx = t.sxa + 16 * ch;
+        const bool xin = sx >= 0 && sx + 16 <= w;
+        if (ro < rpp) {
+            for (int r = ro; r < t.sh; r += rpp) {
+                const int sy = t.sya + r;
+                uint4 v;
+#ifdef WX_NO_STAGE
+                if (true) {
+                    v = make_uint4(sy, sx, r, ch);
+#else
+                if ((unsigned)sy < (unsigned)h && xin) {
+                    v = *reinterpret_cast<const uint4*>(src + (long long)sy * g1_pitch + sx);
+#endif
+                } else {
+                    uint32_t d[4] = {0, 0, 0, 0};
+                    if ((unsigned)sy < (unsigned)h) {
+                        const uint8_t* p = src + (long long)sy * g1_pitch;
+                        for (int i = 0; i < 16; i++) {
+                            const int xx = sx + i;
+                            if ((unsigned)xx < (unsigned)w) d[i >> 2] |= (uint32_t)p[xx] << (8 * (i & 3));
+                        }
+                    }
+                    v = make_uint4(d[0], d[1], d[2], d[3]);
+                }
+                *reinterpret_cast<uint4*>(&s_src[r * kSP + 16 * ch]) = v;
+            }
+        }
+    }
+    __syncthreads();
+    if (nrows == 0) return;
+
+    const double magic = 6755399441055744.0;                 // 1.5 * 2^52
+    const double mX = magic - 32.0 * t.sxa, mY = magic - 32.0 * t.sya;
+    // 32/M8 a power of two -> (X0 + M0*x1) * Wd is exact and fuses with the rounding add
+    const bool pow2 = Wd != 0.0 && (__double_as_longlong(Wd) & 0x000fffffffffffffLL) == 0;
+    const uint32_t bias = 32767u - (uint32_t)thresh;
+    double tx[4], ty[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        tx[k] = M[0] * (4 * cq + k);
+        ty[k] = M[3] * (4 * cq + k);
+        asm volatile("" : "+v"(tx[k]), "+v"(ty[k]));   // keep in registers (no per-row rematerialisation)
+    }
+    lds_d2* xyp = (lds_d2*)(&s_xy[0][0]);
+    lds_u8* srcp = (lds_u8*)(&s_src[0]);
+    if (pow2)
+        warp_rows<true>(xyp, srcp, r0, nrows, y0, xs, g2p, g2_pitch, mp, w, tx, ty, Wd, mX, mY, bias);
+    else
+        warp_rows<false>(xyp, srcp, r0, nrows, y0, xs, g2p, g2_pitch, mp, w, tx, ty, Wd, mX, mY, bias);
 }
 
 hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,
