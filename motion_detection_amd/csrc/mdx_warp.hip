@@ -245,9 +245,19 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
     __shared__ TileInfo s_info;
 
-    const int pair = blockIdx.z;
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs; remap the linear id so
+    // each XCD walks a contiguous run of tiles (row-major), and horizontally adjacent tiles --
+    // which share the 128-B lines of their gray1 footprints and gray2 / mask rows -- meet in
+    // the same L2 at about the same time.
+    const int nbx = gridDim.x, nby = gridDim.y;
+    int bid = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+    {
+        const int total = nbx * nby * gridDim.z, xcd = bid & 7, q8 = total >> 3, r8 = total & 7;
+        bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    }
+    const int pair = bid / (nbx * nby), tile = bid - pair * (nbx * nby);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int x0 = blockIdx.x * kWTile, y0 = blockIdx.y * kHTile;
+    const int x0 = (tile % nbx) * kWTile, y0 = (tile / nbx) * kHTile;
     const int cq = lane & 15, rr = lane >> 4;
     const int xs = x0 + 4 * cq;                     // this lane's 4 columns
     const int r0 = (kHTile / 4) * wave + rr;        // this lane's first tile row

@@ -1,0 +1,38 @@
+"""Turn a scripts/pmc_sets.sh run (FETCH_SIZE / WRITE_SIZE passes over `bench.py --only-roofline`)
+into profiles/pmc_warp_diff.json, the per-launch HBM traffic bench.py reports as roofline.traffic.
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of a wide
+streaming read, so read bytes = 2 * FETCH_SIZE KiB; WRITE_SIZE is exact.
+Usage: python scripts/pmc_to_json.py gpurun_out/pmc_<tag> 3840x2160x32 [out.json]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+d, config = sys.argv[1], sys.argv[2]
+out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_warp_diff.json")
+w, h, b = (int(v) for v in config.split("x"))
+vals = collections.defaultdict(list)
+for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
+    for r in csv.DictReader(open(f)):
+        if "k_warp_diff" not in r["Kernel_Name"]:
+            continue
+        # the roofline launches are the large grids (w*h*b/32 threads for 64x128 tiles of 256)
+        if int(r["Grid_Size"]) < (w * h * b) // 64:
+            continue
+        vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+fetch_kib = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
+write_kib = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
+read_b = 2.0 * fetch_kib * 1024
+write_b = write_kib * 1024
+res = dict(kernel="k_warp_diff", config=config, launches=len(vals["FETCH_SIZE"]),
+           fetch_size_kib=round(fetch_kib, 1), write_size_kib=round(write_kib, 1),
+           read_bytes_per_launch=int(read_b), write_bytes_per_launch=int(write_b),
+           hbm_bytes_per_launch=int(read_b + write_b), algorithmic_bytes_per_launch=3 * w * h * b,
+           correction="read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE",
+           source=os.path.basename(os.path.normpath(d)))
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res))
