@@ -30,33 +30,69 @@ __device__ __forceinline__ int r101(int p, int len)
     return p;
 }
 
+// Front-end kernels (A1, A3, A4) work on aligned 16-byte chunks of each padded row (4 words
+// for the derivative rows): a level's padded columns -40 .. w+39 sit at row bytes 24 .. 64+w+39
+// and every row has >= 16 B of slack after them, so a chunk may spill into the unused margin.
+// Interior chunks take vector loads; chunks that touch a border fall back to per-pixel
+// reflect-101 addressing.  One aligned dwordx4 store per thread.
+struct __attribute__((aligned(4))) u4a4k { uint32_t x, y, z, w; };
+struct __attribute__((aligned(4))) u3a4k { uint32_t x, y, z; };
+struct __attribute__((aligned(4))) u2a4k { uint32_t x, y; };
+
+__device__ __forceinline__ int gray_of(const uint8_t* s, int fmt)
+{
+    // color.cpp RGB2Gray<uchar>, blueIdx 0 on rgb8 data: R gets the blue weight
+    if (fmt == 1) return (s[0] * 1868 + s[1] * 9617 + s[2] * 4899 + 8192) >> 14;
+    return (s[2] * 1868 + s[1] * 9617 + s[0] * 4899 + 8192) >> 14;   // bgr8 -> converted to rgb8 first
+}
+
 // ------------------------------------------------------------------ A1: gray + pad
 // color.cpp RGB2Gray<uchar> with blueIdx 0 on rgb8 data (node.cpp:271 then :50):
 // gray = (R*1868 + G*9617 + B*4899 + 8192) >> 14.  mono8 passes through unchanged.
-// grid: x,y over the padded level-0 image, z = 2*pair + which frame.
+// grid: x -> 16-B chunk of the padded row, y -> padded row, z = 2*pair + which frame.
 __global__ __launch_bounds__(256) void k_gray_pad(const uint8_t* __restrict__ in1, const uint8_t* __restrict__ in2,
                                                   int w, int h, int stride, long long frame_stride, int fmt,
                                                   uint8_t* __restrict__ pyr1, uint8_t* __restrict__ pyr2,
-                                                  long long img_bytes, Level L)
+                                                  long long img_bytes, Level L, int nchunk)
 {
     const int which = blockIdx.z & 1, pair = blockIdx.z >> 1;
-    const int px = blockIdx.x * blockDim.x + threadIdx.x - kPad;
-    const int py = blockIdx.y * blockDim.y + threadIdx.y - kPad;
-    if (px >= w + kPad || py >= h + kPad) return;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x + 1;         // chunk 0 is all margin
+    const int py = blockIdx.y - kPad;
+    if (c > nchunk) return;
     const uint8_t* src = (which ? in2 : in1) + (long long)pair * frame_stride;
-    const int sx = r101(px, w), sy = r101(py, h);
-    const uint8_t* s = src + (long long)sy * stride;
-    int g;
-    if (fmt == 0) {
-        g = s[sx];
+    const uint8_t* s = src + (long long)r101(py, h) * stride;
+    const int px0 = 16 * c - kXOff;
+    uint32_t o[4];
+    if (px0 >= 0 && px0 + 16 <= w && fmt == 0 && (((uintptr_t)(s + px0)) & 3) == 0) {
+        const u4a4k v = *reinterpret_cast<const u4a4k*>(s + px0);
+        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    } else if (px0 >= 0 && px0 + 16 <= w && fmt != 0 && (((uintptr_t)(s + 3 * px0)) & 3) == 0) {
+        uint32_t b[12];
+        const u4a4k* q = reinterpret_cast<const u4a4k*>(s + 3 * px0);
+#pragma unroll
+        for (int t = 0; t < 3; t++) { const u4a4k v = q[t]; b[4 * t] = v.x; b[4 * t + 1] = v.y; b[4 * t + 2] = v.z; b[4 * t + 3] = v.w; }
+        const uint8_t* bb = reinterpret_cast<const uint8_t*>(b);
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            uint32_t d = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) d |= (uint32_t)gray_of(bb + 3 * (4 * t + i), fmt) << (8 * i);
+            o[t] = d;
+        }
     } else {
-        int r, gg, b;
-        if (fmt == 1) { r = s[3 * sx]; gg = s[3 * sx + 1]; b = s[3 * sx + 2]; }
-        else { b = s[3 * sx]; gg = s[3 * sx + 1]; r = s[3 * sx + 2]; }
-        g = (r * 1868 + gg * 9617 + b * 4899 + 8192) >> 14;
+        for (int t = 0; t < 4; t++) {
+            uint32_t d = 0;
+            for (int i = 0; i < 4; i++) {
+                const int px = px0 + 4 * t + i;
+                if (px < -kPad || px >= w + kPad) continue;           // row margin: value unused
+                const int sx = r101(px, w);
+                d |= (uint32_t)(fmt == 0 ? s[sx] : gray_of(s + 3 * sx, fmt)) << (8 * i);
+            }
+            o[t] = d;
+        }
     }
-    uint8_t* dst = (which ? pyr2 : pyr1) + (long long)pair * img_bytes + L.img_off + L.core();
-    dst[(long long)py * L.pitch + px] = (uint8_t)g;
+    uint8_t* row = (which ? pyr2 : pyr1) + (long long)pair * img_bytes + L.img_off + (long long)(py + kPad) * L.pitch;
+    *reinterpret_cast<uint4*>(row + 16 * c) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // ------------------------------------------------------------------ A3/A4: pyrDown
@@ -65,27 +101,64 @@ __global__ __launch_bounds__(256) void k_gray_pad(const uint8_t* __restrict__ in
 // already carries its REFLECT_101 border (>= 2 px), so its taps are read straight from the
 // padded buffer; the destination border is the reflect-101 image of the destination core
 // (copyMakeBorder ... BORDER_REFLECT_101|BORDER_ISOLATED), computed in place.
-__global__ __launch_bounds__(256) void k_pyrdown(uint8_t* __restrict__ pyr1, uint8_t* __restrict__ pyr2,
-                                                 long long img_bytes, Level S, Level D)
+// Per thread 4 destination pixels; each source row segment is one 16-B load and the 5-tap row
+// filter is two chained v_dot4_u32_u8 per output.
+__device__ __forceinline__ uint32_t pyr_px(const uint8_t* src, int sp, int cx, int cy)
 {
-    const int which = blockIdx.z & 1, pair = blockIdx.z >> 1;
-    const int px = blockIdx.x * blockDim.x + threadIdx.x - kPad;
-    const int py = blockIdx.y * blockDim.y + threadIdx.y - kPad;
-    if (px >= D.w + kPad || py >= D.h + kPad) return;
-    uint8_t* slab = (which ? pyr2 : pyr1) + (long long)pair * img_bytes;
-    const uint8_t* src = slab + S.img_off + S.core();
-    const int cx = r101(px, D.w), cy = r101(py, D.h);
-    const uint8_t* s0 = src + (long long)(2 * cy - 2) * S.pitch + (2 * cx - 2);
+    const uint8_t* s0 = src + (long long)(2 * cy - 2) * sp + (2 * cx - 2);
     int acc = 0;
 #pragma unroll
     for (int i = 0; i < 5; i++) {
-        const uint8_t* r = s0 + (long long)i * S.pitch;
-        int hrow = r[2] * 6 + (r[1] + r[3]) * 4 + r[0] + r[4];
-        const int ki = i == 2 ? 6 : (i == 1 || i == 3) ? 4 : 1;
-        acc += hrow * ki;
+        const uint8_t* r = s0 + (long long)i * sp;
+        const int hrow = r[2] * 6 + (r[1] + r[3]) * 4 + r[0] + r[4];
+        acc += hrow * (i == 2 ? 6 : (i == 1 || i == 3) ? 4 : 1);
     }
-    uint8_t* dst = slab + D.img_off + D.core();
-    dst[(long long)py * D.pitch + px] = (uint8_t)((acc + 128) >> 8);
+    return (uint32_t)((acc + 128) >> 8);
+}
+
+__global__ __launch_bounds__(256) void k_pyrdown(uint8_t* __restrict__ pyr1, uint8_t* __restrict__ pyr2,
+                                                 long long img_bytes, Level S, Level D, int nchunk)
+{
+    // 4 destination pixels (one dword) per thread
+    const int which = blockIdx.z & 1, pair = blockIdx.z >> 1;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x + 6;         // dword chunks 0..5 are margin
+    const int py = blockIdx.y - kPad;
+    if (c > nchunk) return;
+    uint8_t* slab = (which ? pyr2 : pyr1) + (long long)pair * img_bytes;
+    const uint8_t* src = slab + S.img_off + S.core();
+    const int px0 = 4 * c - kXOff;
+    const int cy = r101(py, D.h);
+    uint32_t o = 0;
+    if (px0 >= 0 && px0 + 4 <= D.w) {
+        // source columns 2*px0-4 .. 2*px0+11: one 16-B load per row (4-B aligned)
+        const uint8_t* s0 = src + (long long)(2 * cy - 2) * S.pitch + (2 * px0 - 4);
+        uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const u4a4k a = *reinterpret_cast<const u4a4k*>(s0 + (long long)i * S.pitch);
+            const uint32_t wd[4] = {a.x, a.y, a.z, a.w};
+            const uint32_t ki = i == 2 ? 6u : (i == 1 || i == 3) ? 4u : 1u;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                // taps at bytes 2j+2 .. 2j+6 of the segment
+                const int b0 = 2 * j + 2, q = b0 >> 2;
+                const uint32_t lo = (b0 & 3) ? __builtin_amdgcn_alignbit(wd[q + 1], wd[q], 16) : wd[q];
+                const uint32_t hi = (b0 & 3) ? (wd[q + 1] >> 16) : wd[q + 1];
+                const uint32_t hrow = __builtin_amdgcn_udot4(hi, 1u, __builtin_amdgcn_udot4(lo, 0x04060401u, 0u, false), false);
+                acc[j] += hrow * ki;
+            }
+        }
+        o = ((acc[0] + 128) >> 8) | (((acc[1] + 128) >> 8) << 8) | (((acc[2] + 128) >> 8) << 16) |
+            (((acc[3] + 128) >> 8) << 24);
+    } else {
+        for (int i = 0; i < 4; i++) {
+            const int px = px0 + i;
+            if (px < -kPad || px >= D.w + kPad) continue;             // row margin: value unused
+            o |= pyr_px(src, S.pitch, r101(px, D.w), cy) << (8 * i);
+        }
+    }
+    uint8_t* row = slab + D.img_off + (long long)(py + kPad) * D.pitch;
+    *reinterpret_cast<uint32_t*>(row + 4 * c) = o;
 }
 
 // ------------------------------------------------------------------ A3: Scharr derivs
@@ -93,26 +166,42 @@ __global__ __launch_bounds__(256) void k_pyrdown(uint8_t* __restrict__ pyr1, uin
 // Ix = t0[x+1]-t0[x-1], Iy = 3(t1[x-1]+t1[x+1])+10 t1[x].  OpenCV clamps the row/col
 // neighbours as reflect-101 (row -1 -> 1, col cols -> cols-2), which is exactly the padded
 // level's border, so the stencil reads the padded image directly.  Border = 0
-// (copyMakeBorder ... BORDER_CONSTANT).
+// (copyMakeBorder ... BORDER_CONSTANT).  Per thread 4 pixels (one 16-B store); each of the
+// three source rows is one dwordx3 load of bytes x0-4 .. x0+7.
 __global__ __launch_bounds__(256) void k_scharr(const uint8_t* __restrict__ pyr1, uint32_t* __restrict__ der,
-                                                long long img_bytes, long long der_words, Level L)
+                                                long long img_bytes, long long der_words, Level L, int nchunk)
 {
     const int pair = blockIdx.z;
-    const int px = blockIdx.x * blockDim.x + threadIdx.x - kPad;
-    const int py = blockIdx.y * blockDim.y + threadIdx.y - kPad;
-    if (px >= L.w + kPad || py >= L.h + kPad) return;
-    uint32_t* d = der + (long long)pair * der_words + L.der_off + L.core() + (long long)py * L.pitch + px;
-    if (px < 0 || py < 0 || px >= L.w || py >= L.h) { *d = 0u; return; }
-    const uint8_t* s = pyr1 + (long long)pair * img_bytes + L.img_off + L.core() + (long long)py * L.pitch + px;
-    const int p = L.pitch;
-    int t0m = (s[-p - 1] + s[p - 1]) * 3 + s[-1] * 10;
-    int t0p = (s[-p + 1] + s[p + 1]) * 3 + s[1] * 10;
-    int t1m = s[p - 1] - s[-p - 1];
-    int t1c = s[p] - s[-p];
-    int t1p = s[p + 1] - s[-p + 1];
-    int ix = t0p - t0m;
-    int iy = (t1m + t1p) * 3 + t1c * 10;
-    *d = (uint32_t)(uint16_t)(int16_t)ix | ((uint32_t)(uint16_t)(int16_t)iy << 16);
+    const int c = blockIdx.x * blockDim.x + threadIdx.x + 4;         // word chunks 0..3 are margin
+    const int py = blockIdx.y - kPad;
+    if (c > nchunk) return;
+    const int px0 = 4 * c - kXOff;
+    uint32_t o[4] = {0, 0, 0, 0};
+    if (py >= 0 && py < L.h && px0 + 4 > 0 && px0 < L.w) {
+        const uint8_t* s = pyr1 + (long long)pair * img_bytes + L.img_off + L.core() + (long long)py * L.pitch + px0 - 4;
+        const int p = L.pitch;
+        uint32_t rw[3][3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const u3a4k v = *reinterpret_cast<const u3a4k*>(s + (long long)(r - 1) * p);
+            rw[r][0] = v.x; rw[r][1] = v.y; rw[r][2] = v.z;
+        }
+        auto B = [&](int r, int b) -> int { return (int)((rw[r][b >> 2] >> (8 * (b & 3))) & 255u); };
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int px = px0 + i;
+            if (px < 0 || px >= L.w) continue;
+            const int bm = 3 + i, bc = 4 + i, bp = 5 + i;               // bytes x-1, x, x+1
+            const int t0m = (B(0, bm) + B(2, bm)) * 3 + B(1, bm) * 10;
+            const int t0p = (B(0, bp) + B(2, bp)) * 3 + B(1, bp) * 10;
+            const int t1m = B(2, bm) - B(0, bm), t1c = B(2, bc) - B(0, bc), t1p = B(2, bp) - B(0, bp);
+            const int ix = t0p - t0m;
+            const int iy = (t1m + t1p) * 3 + t1c * 10;
+            o[i] = (uint32_t)(uint16_t)(int16_t)ix | ((uint32_t)(uint16_t)(int16_t)iy << 16);
+        }
+    }
+    uint32_t* row = der + (long long)pair * der_words + L.der_off + (long long)(py + kPad) * L.pitch;
+    *reinterpret_cast<uint4*>(row + 4 * c) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // ------------------------------------------------------------------ A5: LK tracker
@@ -642,34 +731,34 @@ __global__ void k_export_fit(const PairFit* __restrict__ fits, int batch, double
 // A8-A10 (warp + absdiff + threshold) lives in mdx_warp.hip.
 
 // ------------------------------------------------------------------ launchers
-static inline dim3 padded_grid(int w, int h, int z, dim3 blk)
-{
-    return dim3((w + 2 * kPad + blk.x - 1) / blk.x, (h + 2 * kPad + blk.y - 1) / blk.y, z);
-}
+// last 16-B chunk index of a padded row (columns -40 .. w+39 at row bytes 24 .. 64+w+39)
+static inline int last_chunk16(int w) { return (kXOff + w + kPad - 1) / 16; }
 
 hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const uint8_t* in2, int w, int h, int stride,
                            long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g)
 {
-    const dim3 blk(64, 4);
-    hipLaunchKernelGGL(k_gray_pad, padded_grid(w, h, 2 * batch, blk), blk, 0, s, in1, in2, w, h, stride, frame_stride,
-                       fmt, pyr1, pyr2, g.img_bytes, g.lv[0]);
+    const int nchunk = last_chunk16(w);
+    const dim3 grid((nchunk + 63) / 64, h + 2 * kPad, 2 * batch);
+    hipLaunchKernelGGL(k_gray_pad, grid, dim3(64), 0, s, in1, in2, w, h, stride, frame_stride, fmt, pyr1, pyr2,
+                       g.img_bytes, g.lv[0], nchunk);
     return hipGetLastError();
 }
 
 hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level)
 {
-    const dim3 blk(64, 4);
     const Level& D = g.lv[level];
-    hipLaunchKernelGGL(k_pyrdown, padded_grid(D.w, D.h, 2 * batch, blk), blk, 0, s, pyr1, pyr2, g.img_bytes,
-                       g.lv[level - 1], D);
+    const int nchunk = (kXOff + D.w + kPad - 1) / 4;                 // last dword chunk
+    const dim3 grid((nchunk - 6 + 1 + 63) / 64, D.h + 2 * kPad, 2 * batch);
+    hipLaunchKernelGGL(k_pyrdown, grid, dim3(64), 0, s, pyr1, pyr2, g.img_bytes, g.lv[level - 1], D, nchunk);
     return hipGetLastError();
 }
 
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level)
 {
-    const dim3 blk(64, 4);
     const Level& L = g.lv[level];
-    hipLaunchKernelGGL(k_scharr, padded_grid(L.w, L.h, batch, blk), blk, 0, s, pyr1, der, g.img_bytes, g.der_words, L);
+    const int nchunk = (kXOff + L.w + kPad - 1) / 4;                 // last 4-word chunk
+    const dim3 grid((nchunk - 4 + 1 + 63) / 64, L.h + 2 * kPad, batch);
+    hipLaunchKernelGGL(k_scharr, grid, dim3(64), 0, s, pyr1, der, g.img_bytes, g.der_words, L, nchunk);
     return hipGetLastError();
 }
 

@@ -81,13 +81,34 @@ __device__ __forceinline__ uint32_t quad_bcast_u(uint32_t v)
 // 4-B aligned column B = inx & ~3 cover every lane's taps (lane k needs bytes o + 4g and
 // o + 4g + 1 with o = (inx & 3) + k <= 6, i.e. inside dwords g, g+1).  Each lane loads 3 of
 // them and DPP broadcasts assemble the row in every lane: 12 B of L1 traffic per lane, not 48.
-__device__ __forceinline__ void load_jrow_quad(const uint32_t* seg, int k, uint32_t (&r)[11])
+__device__ __forceinline__ u3a4 load_jrow_part(const uint32_t* seg, int k)
 {
-    const u3a4 m = *reinterpret_cast<const u3a4*>(seg + 3 * k);
+    return *reinterpret_cast<const u3a4*>(seg + 3 * k);
+}
+__device__ __forceinline__ void bcast_jrow(const u3a4 m, uint32_t (&r)[11])
+{
     r[0] = quad_bcast_u<0>(m.x); r[1] = quad_bcast_u<0>(m.y); r[2] = quad_bcast_u<0>(m.z);
     r[3] = quad_bcast_u<1>(m.x); r[4] = quad_bcast_u<1>(m.y); r[5] = quad_bcast_u<1>(m.z);
     r[6] = quad_bcast_u<2>(m.x); r[7] = quad_bcast_u<2>(m.y); r[8] = quad_bcast_u<2>(m.z);
     r[9] = quad_bcast_u<3>(m.x); r[10] = quad_bcast_u<3>(m.y);
+}
+__device__ __forceinline__ void load_jrow_quad(const uint32_t* seg, int k, uint32_t (&r)[11])
+{
+    bcast_jrow(load_jrow_part(seg, k), r);
+}
+
+// Ordering point between a window row's LDS staging writes and the next row's reads.  A
+// workgroup is one wave and one wave's LDS instructions execute in order, so only the compiler
+// must be kept from moving LDS accesses across it (no s_barrier, no forced vmcnt(0)).
+__device__ __forceinline__ void wave_lds_fence()
+{
+#ifdef LKX_SYNC
+    __syncthreads();
+#else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
 }
 
 // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs; remap so that each
@@ -157,7 +178,12 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
 // separate launches from maxLevel down to 0; the position carried between them is next_pts
 // (the reference's nextPts[ptidx], stored every level).
 template <int NCH>
-__global__ __launch_bounds__(64) void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
+#ifdef LKX_WPE   // timing variants: occupancy request
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE, 8)))
+#else
+__global__ __launch_bounds__(64)
+#endif
+void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
 {
     constexpr int UW = NCH * 128;           // union columns per group
     constexpr float HALFW = 19.5f;
@@ -244,7 +270,7 @@ __global__ __launch_bounds__(64) void k_lk_level(LkArgs a, const uint8_t* __rest
         float s12 = 0.f;
         gload(v0, false);
         lstore(0, false);
-        __syncthreads();
+        wave_lds_fence();
 #pragma unroll 2
         for (int y = 0; y < kWin; y++) {
             const int buf = y & 1;
@@ -258,7 +284,7 @@ __global__ __launch_bounds__(64) void k_lk_level(LkArgs a, const uint8_t* __rest
                 s12 = s12 + f.x * f.y;           // Ix*Iy
             }
             if (y + 1 < kWin) lstore(buf ^ 1, false);
-            __syncthreads();
+            wave_lds_fence();
         }
         const float a11 = ((quad_bcast<0>(sd.x) + quad_bcast<1>(sd.x)) + quad_bcast<2>(sd.x)) + quad_bcast<3>(sd.x);
         const float a12 = ((quad_bcast<0>(s12) + quad_bcast<1>(s12)) + quad_bcast<2>(s12)) + quad_bcast<3>(s12);
@@ -320,14 +346,26 @@ __global__ __launch_bounds__(64) void k_lk_level(LkArgs a, const uint8_t* __rest
         }
         gload(v0, true);
         lstore(0, true);
-        __syncthreads();
+        wave_lds_fence();
+#ifdef LKX_JPF
+        // J rows are prefetched one row ahead (the DPP broadcast needs the data at once)
+        jrow += jstride;
+        u3a4 jnext = load_jrow_part(jrow, k);
+#endif
 #pragma unroll 2
         for (int y = 0; y < kWin; y++) {
             const int buf = y & 1;
             if (y + 1 < kWin) gload(v0 + y + 1, true);
-            jrow += jstride;
             uint32_t rj[11];
+#ifdef LKX_JPF
+            const u3a4 jcur = jnext;
+            jrow += jstride;
+            if (y + 1 < kWin) jnext = load_jrow_part(jrow, k);
+            bcast_jrow(jcur, rj);
+#else
+            jrow += jstride;
             load_jrow_quad(jrow, k, rj);
+#endif
             const uint32_t* ld = lD0 + buf * LBUF;
             const uint32_t* lc = lC0 + buf * LBUF;
 #pragma unroll
@@ -343,7 +381,7 @@ __global__ __launch_bounds__(64) void k_lk_level(LkArgs a, const uint8_t* __rest
                 pa[g] = pb[g];
             }
             if (y + 1 < kWin) lstore(buf ^ 1, true);
-            __syncthreads();
+            wave_lds_fence();
         }
         if (!act) acc = f2{0.f, 0.f};
         // b = (P0+P2) + (P1+P3) across the quad; inactive quads compute garbage they ignore
