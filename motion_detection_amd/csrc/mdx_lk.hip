@@ -44,6 +44,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // 4-B aligned multi-dword loads (global_load_dwordx4/x3 at dword-aligned addresses)
 struct __attribute__((aligned(4))) u4a4 { uint32_t x, y, z, w; };
 struct __attribute__((aligned(4))) u3a4 { uint32_t x, y, z; };
+struct __attribute__((aligned(4))) u2a4 { uint32_t x, y; };
 
 // residue-class tables: [level][axis][128]
 __device__ __forceinline__ int class_of(const int16_t* cmap, int level, int axis, int res)
@@ -134,7 +135,9 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
     const int pair = blockIdx.z / nclass, cls = blockIdx.z % nclass;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int v = blockIdx.y;
-    if (4 * j >= C.PW || v >= C.UH) return;
+    // columns a window can reach: x = u - 40 <= w + 38; the rest of PW is union-load slack whose
+    // values no lane uses, so it is left unwritten
+    if (4 * j >= a.g.lv[level].w + 2 * kPad || v >= C.UH) return;
     const Level L = a.g.lv[level];
     const float scale = (float)(1. / (1 << level));
     const int rx = residue_of(a.rlist, level, 0, cls % C.nrx), ry = residue_of(a.rlist, level, 1, cls / C.nrx);
@@ -147,25 +150,40 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
     const int y = v - kPad;
     const int p = L.pitch;
     uint8_t* base = cls_out + (long long)pair * a.plan.bytes_per_pair + C.off + (long long)cls * C.class_bytes;
-    uint32_t dv[4];
+    uint32_t dv[4] = {0, 0, 0, 0};
     int cv[4];
+    const int x0 = 4 * j - kPad;                     // first of this thread's 4 columns
+    if (y < L.h + kPad - 1 && x0 < L.w + kPad - 1) {
+        // rows y, y+1 of the padded level: 5 image bytes (one 8-B load) and 5 derivative words
+        // (16-B + 4-B loads) per row; x0 is a multiple of 4 and the core is 64-B aligned
+        const uint8_t* ip = I + (long long)y * p + x0;
+        const uint32_t* dp = D + (long long)y * p + x0;
+        uint32_t ib[2][2], dw[2][5];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int x = 4 * j + q - kPad;
-        dv[q] = 0;
-        int ival = 0;
-        if (x < L.w + kPad - 1 && y < L.h + kPad - 1) {
-            const uint8_t* ip = I + (long long)y * p + x;
-            ival = (ip[0] * w00 + ip[1] * w01 + ip[p] * w10 + ip[p + 1] * w11 + 256) >> 9;
-            const uint32_t* dp = D + (long long)y * p + x;
-            const uint32_t d00 = dp[0], d01 = dp[1], d10 = dp[p], d11 = dp[p + 1];
+        for (int r = 0; r < 2; r++) {
+            const u2a4 bi = *reinterpret_cast<const u2a4*>(ip + (long long)r * p);
+            ib[r][0] = bi.x; ib[r][1] = bi.y;
+            const uint4 d4 = *reinterpret_cast<const uint4*>(dp + (long long)r * p);
+            dw[r][0] = d4.x; dw[r][1] = d4.y; dw[r][2] = d4.z; dw[r][3] = d4.w;
+            dw[r][4] = dp[(long long)r * p + 4];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (x0 + q >= L.w + kPad - 1) { cv[q] = 256; continue; }
+            const int i00 = (ib[0][q >> 2] >> (8 * (q & 3))) & 255, i01 = (ib[0][(q + 1) >> 2] >> (8 * ((q + 1) & 3))) & 255;
+            const int i10 = (ib[1][q >> 2] >> (8 * (q & 3))) & 255, i11 = (ib[1][(q + 1) >> 2] >> (8 * ((q + 1) & 3))) & 255;
+            const int ival = (i00 * w00 + i01 * w01 + i10 * w10 + i11 * w11 + 256) >> 9;
+            const uint32_t d00 = dw[0][q], d01 = dw[0][q + 1], d10 = dw[1][q], d11 = dw[1][q + 1];
             const int ixv = ((int)(int16_t)d00 * w00 + (int)(int16_t)d01 * w01 + (int)(int16_t)d10 * w10 +
                              (int)(int16_t)d11 * w11 + 8192) >> 14;
             const int iyv = (((int)d00 >> 16) * w00 + ((int)d01 >> 16) * w01 + ((int)d10 >> 16) * w10 +
                              ((int)d11 >> 16) * w11 + 8192) >> 14;
             dv[q] = ((uint32_t)ixv & 0xffffu) | ((uint32_t)iyv << 16);
+            cv[q] = 256 - 512 * ival;   // J-chain bias: (S + C) >> 9 == ((S + 256) >> 9) - I
         }
-        cv[q] = 256 - 512 * ival;   // J-chain bias: (S + C) >> 9 == ((S + 256) >> 9) - I
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++) cv[q] = 256;
     }
     const long long o = (long long)v * C.PW + 4 * j;
     *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(base) + o) = make_uint4(dv[0], dv[1], dv[2], dv[3]);
@@ -437,7 +455,7 @@ hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint8_t* cls)
         ca.plan = a.plan;
         ca.rlist = a.rlist;
         ca.level = l;
-        const dim3 grid((C.PW / 4 + 63) / 64, C.UH, batch * C.nrx * C.nry);
+        const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.UH, batch * C.nrx * C.nry);
         hipLaunchKernelGGL(k_lk_class, grid, dim3(64), 0, s, a.pyr1, a.der, cls, ca);
         const dim3 lg(((C.nxp + 15) / 16) * a.ny, batch);
         switch (a.plan.nch) {
