@@ -34,6 +34,7 @@ struct mdx_ctx {
     DevBuf bnp, bst;                         // LK outputs the batched caller did not ask for
     DevBuf cls, Abuf, ctab;                  // LK v2: class planes, A sums, residue tables
     DevBuf dbg;                              // LK v2 per-level trace (MDX_LK_DEBUG=1)
+    DevBuf csum;                             // classify: per-block summaries
     bool lk_debug = false;
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
     int plan_w = -1, plan_h = -1, plan_ps = -1, plan_ml = -1;
@@ -277,7 +278,7 @@ extern "C" int mdx_destroy(mdx_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->pyr1, &c->pyr2, &c->der, &c->fits, &c->in1, &c->in2, &c->np, &c->st,
                       &c->vec, &c->mask, &c->H, &c->Hext, &c->num, &c->bnp, &c->bst,
-                      &c->cls, &c->Abuf, &c->ctab, &c->dbg};
+                      &c->cls, &c->Abuf, &c->ctab, &c->dbg, &c->csum};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (c->ev) {
@@ -439,8 +440,9 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         }
     }
     mark(c, 4);
+    if ((rc = ensure(c, c->csum, classify_scratch_bytes(batch, npts))) != MDX_OK) return rc;
     HIP_OR_RETURN(c, launch_classify_fit(s, batch, d_np, d_st, npts, ny, P.pixel_step, P.min_vector_size, d_vec, fits,
-                                         P.fit_mode, d_Hext));
+                                         P.fit_mode, d_Hext, c->csum.p));
     mark(c, 5);
     if (d_mask) {
         const Level& L0 = g.lv[0];

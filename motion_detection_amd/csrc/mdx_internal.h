@@ -96,7 +96,9 @@ hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
 hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint8_t* cls);
 hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
                                int ny, int pixel_step, double min_vector_size, double* vectors, PairFit* fits,
-                               int fit_mode, const double* H_external);
+                               int fit_mode, const double* H_external, void* scratch);
+// bytes of the scratch launch_classify_fit needs
+inline size_t classify_scratch_bytes(int batch, int npts) { return (size_t)batch * ((npts + 255) / 256) * 32; }
 hipError_t launch_set_fit_external(hipStream_t s, int batch, const double* H_external, PairFit* fits);
 hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,
                             const uint8_t* g2, long long g2_stride, int g2_pitch, int w, int h,

@@ -9,7 +9,7 @@
 //   A3/A4   k_pyrdown        pyrDown + REFLECT_101 padding, both frames of every pair
 //   A3      k_scharr         calcSharrDeriv + CONSTANT-0 padding (prev frame)
 //   A5      k_lk             calcOpticalFlowPyrLK (LKTrackerInvoker, SSE2 summation order)
-//   A6/A7   k_classify_fit   Vec4d classification, first-4 getPerspectiveTransform, invert
+//   A6/A7   k_classify/k_fit Vec4d classification, first-4 getPerspectiveTransform, invert
 //   A8-A10  k_warp_diff      warpPerspective + absdiff + threshold, fused (mdx_warp.hip)
 #include "mdx_internal.h"
 
@@ -637,75 +637,111 @@ __device__ void dev_invert3x3(const double* m, double* out)
 // vectors, pick the first four accepted in x-major order, fit and invert.  One 256-thread
 // workgroup per pair; the first-4 search is a ballot scan that stops as soon as 4 are found
 // (only the count needs the full sweep).
-__global__ __launch_bounds__(256) void k_classify_fit(const float* __restrict__ next_pts, const uint8_t* __restrict__ status,
-                                                      int npts, int ny, int pixel_step, double mvs,
-                                                      double* __restrict__ vectors, PairFit* __restrict__ fits,
-                                                      int fit_mode, const double* __restrict__ H_ext)
+// Two kernels.  k_classify: one 256-point block per workgroup writes the Vec4d of its points
+// and a summary {accepted count, first four accepted indices in block order}.  k_fit: one wave
+// per pair prefix-sums the block counts (x-major block order = the reference's point order),
+// picks the first four accepted points overall and runs the fit on lane 0.
+struct BlockSummary {
+    int count;
+    int first[4];
+    int pad_[3];
+};
+
+__global__ __launch_bounds__(256) void k_classify(const float* __restrict__ next_pts, const uint8_t* __restrict__ status,
+                                                  int npts, int ny, int pixel_step, double mvs,
+                                                  double* __restrict__ vectors, BlockSummary* __restrict__ summ)
 {
-    const int pair = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    __shared__ float s_src[8], s_dst[8];
+    const int pair = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     __shared__ int s_wcnt[4];
-    __shared__ int s_total;
-    if (tid == 0) s_total = 0;
-    __syncthreads();
-    const float* np = next_pts + (long long)pair * npts * 2;
-    const uint8_t* st = status + (long long)pair * npts;
-    for (int base = 0; base < npts; base += 256) {
-        const int i = base + tid;
-        bool acc = false;
-        float sx = 0.f, sy = 0.f, ex = 0.f, ey = 0.f;
-        if (i < npts) {
-            sx = (float)((i / ny) * pixel_step);
-            sy = (float)((i % ny) * pixel_step);
-            ex = np[2 * i];
-            ey = np[2 * i + 1];
-            double v0, v1, v2, v3;
-            if (st[i]) {
-                const float xd = ex - sx, yd = ey - sy;
-                if (fabs((double)fabsf(xd)) > mvs || fabs((double)fabsf(yd)) > mvs) {
-                    acc = true;
-                    v0 = sx; v1 = sy; v2 = xd; v3 = yd;
-                } else {
-                    v0 = sx; v1 = sy; v2 = 0.0; v3 = 0.0;
-                }
+    const int i = blk * 256 + tid;
+    bool acc = false;
+    if (i < npts) {
+        const float sx = (float)((i / ny) * pixel_step), sy = (float)((i % ny) * pixel_step);
+        const float2 e = reinterpret_cast<const float2*>(next_pts)[(long long)pair * npts + i];
+        double v0, v1, v2, v3;
+        if (status[(long long)pair * npts + i]) {
+            const float xd = e.x - sx, yd = e.y - sy;       // float differences (:82-83)
+            if (fabs((double)fabsf(xd)) > mvs || fabs((double)fabsf(yd)) > mvs) {
+                acc = true;
+                v0 = sx; v1 = sy; v2 = xd; v3 = yd;
             } else {
-                v0 = -1.0; v1 = -1.0; v2 = 0.0; v3 = 0.0;
+                v0 = sx; v1 = sy; v2 = 0.0; v3 = 0.0;
             }
-            if (vectors) {
-                double* v = vectors + ((long long)pair * npts + i) * 4;
-                v[0] = v0; v[1] = v1; v[2] = v2; v[3] = v3;
-            }
-        }
-        const unsigned long long bal = __ballot(acc);
-        if (lane == 0) s_wcnt[wave] = __popcll(bal);
-        __syncthreads();
-        int before = s_total;
-        for (int w2 = 0; w2 < wave; w2++) before += s_wcnt[w2];
-        const int rank = before + __popcll(bal & ((1ull << lane) - 1ull));
-        if (acc && rank < 4) {
-            s_src[2 * rank] = sx; s_src[2 * rank + 1] = sy;
-            s_dst[2 * rank] = ex; s_dst[2 * rank + 1] = ey;
-        }
-        __syncthreads();
-        if (tid == 0) s_total += s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
-        __syncthreads();
-    }
-    if (tid == 0) {
-        PairFit& f = fits[pair];
-        const int total = s_total;
-        f.num_vectors = total;
-        if (fit_mode == 1) {
-            for (int k = 0; k < 9; k++) f.H[k] = H_ext[(long long)pair * 9 + k];
-            dev_invert3x3(f.H, f.Hinv);
-            f.fit_status = 0;
-        } else if (total >= 4) {
-            dev_perspective_fit(s_src, s_dst, f.H);
-            dev_invert3x3(f.H, f.Hinv);
-            f.fit_status = 0;
         } else {
-            for (int k = 0; k < 9; k++) { f.H[k] = 0.0; f.Hinv[k] = 0.0; }
-            f.fit_status = total == 0 ? 1 : 2;
+            v0 = -1.0; v1 = -1.0; v2 = 0.0; v3 = 0.0;
         }
+        if (vectors) {
+            double4* v = reinterpret_cast<double4*>(vectors) + (long long)pair * npts + i;
+            *v = make_double4(v0, v1, v2, v3);
+        }
+    }
+    const unsigned long long bal = __ballot(acc);
+    if (lane == 0) s_wcnt[wave] = __popcll(bal);
+    __syncthreads();
+    int before = 0;
+    for (int w2 = 0; w2 < wave; w2++) before += s_wcnt[w2];
+    const int rank = before + __popcll(bal & ((1ull << lane) - 1ull));
+    BlockSummary& S = summ[(long long)pair * gridDim.x + blk];
+    if (acc && rank < 4) S.first[rank] = i;
+    if (tid == 0) S.count = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+}
+
+__global__ __launch_bounds__(64) void k_fit(const float* __restrict__ next_pts, int npts, int ny, int pixel_step,
+                                            const BlockSummary* __restrict__ summ, int nblk, PairFit* __restrict__ fits,
+                                            int fit_mode, const double* __restrict__ H_ext)
+{
+    const int pair = blockIdx.x, lane = threadIdx.x;
+    const BlockSummary* S = summ + (long long)pair * nblk;
+    int carry = 0;          // accepted points in blocks before the current chunk
+    int pick[4] = {-1, -1, -1, -1};
+    for (int b0 = 0; b0 < nblk; b0 += 64) {
+        const int b = b0 + lane;
+        const int cnt = b < nblk ? S[b].count : 0;
+        int incl = cnt;     // inclusive prefix over the chunk
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        const int excl = carry + incl - cnt;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            // the block holding overall rank r (one lane at most), then broadcast its index
+            const bool here = cnt > 0 && r >= excl && r < excl + cnt;
+            const unsigned long long m = __ballot(here);
+            if (m) {
+                const int src = __ffsll((long long)m) - 1;
+                const int v = here ? S[b].first[r - excl] : 0;
+                const int got = __shfl(v, src);
+                if (pick[r] < 0) pick[r] = got;
+            }
+        }
+        carry += __shfl(incl, 63);
+    }
+    if (lane != 0) return;
+    PairFit& f = fits[pair];
+    const int total = carry;
+    f.num_vectors = total;
+    if (fit_mode == 1) {
+        for (int k = 0; k < 9; k++) f.H[k] = H_ext[(long long)pair * 9 + k];
+        dev_invert3x3(f.H, f.Hinv);
+        f.fit_status = 0;
+    } else if (total >= 4) {
+        float src[8], dst[8];
+        for (int r = 0; r < 4; r++) {
+            const int i = pick[r];
+            src[2 * r] = (float)((i / ny) * pixel_step);
+            src[2 * r + 1] = (float)((i % ny) * pixel_step);
+            const float2 e = reinterpret_cast<const float2*>(next_pts)[(long long)pair * npts + i];
+            dst[2 * r] = e.x;
+            dst[2 * r + 1] = e.y;
+        }
+        dev_perspective_fit(src, dst, f.H);
+        dev_invert3x3(f.H, f.Hinv);
+        f.fit_status = 0;
+    } else {
+        for (int k = 0; k < 9; k++) { f.H[k] = 0.0; f.Hinv[k] = 0.0; }
+        f.fit_status = total == 0 ? 1 : 2;
     }
 }
 
@@ -772,10 +808,14 @@ hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a)
 
 hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
                                int ny, int pixel_step, double mvs, double* vectors, PairFit* fits, int fit_mode,
-                               const double* H_external)
+                               const double* H_external, void* scratch)
 {
-    hipLaunchKernelGGL(k_classify_fit, dim3(batch), dim3(256), 0, s, next_pts, status, npts, ny, pixel_step, mvs,
-                       vectors, fits, fit_mode, H_external);
+    const int nblk = (npts + 255) / 256;
+    BlockSummary* summ = reinterpret_cast<BlockSummary*>(scratch);
+    hipLaunchKernelGGL(k_classify, dim3(nblk, batch), dim3(256), 0, s, next_pts, status, npts, ny, pixel_step, mvs,
+                       vectors, summ);
+    hipLaunchKernelGGL(k_fit, dim3(batch), dim3(64), 0, s, next_pts, npts, ny, pixel_step, summ, nblk, fits, fit_mode,
+                       H_external);
     return hipGetLastError();
 }
 
