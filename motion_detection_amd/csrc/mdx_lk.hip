@@ -45,6 +45,15 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 struct __attribute__((aligned(4))) u4a4 { uint32_t x, y, z, w; };
 struct __attribute__((aligned(4))) u3a4 { uint32_t x, y, z; };
 struct __attribute__((aligned(4))) u2a4 { uint32_t x, y; };
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v3u __attribute__((ext_vector_type(3)));
+// raw buffer descriptor over [base, base + bytes) (cdna_hip_programming.md T8: built from
+// wave-uniform values only); loads then take a 32-bit per-lane byte offset
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, long long bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                             (int)min(bytes, (long long)0x7fffffff), 0x00020000);
+}
 
 // residue-class tables: [level][axis][128]
 __device__ __forceinline__ int class_of(const int16_t* cmap, int level, int axis, int res)
@@ -243,7 +252,14 @@ void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
     const int ub = min(max(ipx0 + kPad, 0), C.PW - UW);          // union start column
     const int off = min(max(ipx + kPad - ub, 0), UW - kWin);     // this point's column in it
     const uint32_t* gD = reinterpret_cast<const uint32_t*>(cbase) + ub + 4 * gl;
-    const uint32_t* gC = gD + (long long)C.UH * C.PW;
+    [[maybe_unused]] const uint32_t* gC = gD + (long long)C.UH * C.PW;
+    // buffer addressing: descriptor over this pair's class slab, 32-bit lane offsets; the C
+    // array sits a constant UH*PW*4 bytes after D (scalar offset field)
+    const uint8_t* cslab = cls + (long long)pair * a.plan.bytes_per_pair;
+    const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cslab, a.plan.bytes_per_pair);
+    const uint32_t dlane = (uint32_t)(reinterpret_cast<const uint8_t*>(gD) - cslab);
+    const int csoff = C.UH * C.PW * 4;
+    const uint32_t rowb = (uint32_t)C.PW * 4;
     const int v0 = min(max(ipy + kPad, 0), C.UH - kWin);          // first window row (wave-uniform)
     const uint32_t* lD0 = &lds[0][grp][0][off + k];
     const uint32_t* lC0 = &lds[0][grp][1][off + k];
@@ -265,12 +281,22 @@ void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
     auto gload = [&](int v, bool withC) {
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
+#ifdef LKX_NOBUF
             const u4a4 t = *reinterpret_cast<const u4a4*>(gD + (long long)v * C.PW + 128 * c);
             rd[c] = make_uint4(t.x, t.y, t.z, t.w);
             if (withC) {
                 const u4a4 s = *reinterpret_cast<const u4a4*>(gC + (long long)v * C.PW + 128 * c);
                 rc[c] = make_uint4(s.x, s.y, s.z, s.w);
             }
+#else
+            const uint32_t vo = dlane + (uint32_t)v * rowb + 512u * c;
+            const v4u t = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)vo, 0, 0);
+            rd[c] = make_uint4(t.x, t.y, t.z, t.w);
+            if (withC) {
+                const v4u q = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)vo, csoff, 0);
+                rc[c] = make_uint4(q.x, q.y, q.z, q.w);
+            }
+#endif
         }
     };
     auto lstore = [&](int buf, bool withC) {
@@ -327,6 +353,8 @@ void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
     // ---- Newton iterations
     const int pitch = L.pitch;
     const uint8_t* Jb = a.pyr2 + (long long)pair * a.g.img_bytes + L.img_off + L.core();
+    const __amdgpu_buffer_rsrc_t jrs = buf_rsrc(a.pyr2 + (long long)pair * a.g.img_bytes, a.g.img_bytes);
+    const uint32_t jbase = (uint32_t)(L.img_off + L.core());
     float nx = npx - HALFW, ny = npy - HALFW;
     float pdx = 0.f, pdy = 0.f;
     bool act = ok;
@@ -353,7 +381,8 @@ void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
         const int o = (inx & 3) + k;
         const unsigned sel = (unsigned)o | 0x0c00u | ((unsigned)(o + 1) << 16) | 0x0c000000u;
         const uint32_t* jrow = reinterpret_cast<const uint32_t*>(Jb + (long long)iny * pitch + (inx & ~3));
-        const int jstride = pitch >> 2;
+        [[maybe_unused]] const int jstride = pitch >> 2;
+        uint32_t joff = jbase + (uint32_t)(iny * pitch + (inx & ~3) + 12 * k);   // buffer offset of this lane's J dwords
         // taps of the current window row (pa) are the previous row's lower taps (pb)
         s2 pa[10], pb[10];
         {
@@ -380,9 +409,17 @@ void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
             jrow += jstride;
             if (y + 1 < kWin) jnext = load_jrow_part(jrow, k);
             bcast_jrow(jcur, rj);
-#else
+#elif defined(LKX_NOBUF)
             jrow += jstride;
             load_jrow_quad(jrow, k, rj);
+#else
+            joff += (uint32_t)pitch;
+            {
+                const v3u m = __builtin_amdgcn_raw_buffer_load_b96(jrs, (int)joff, 0, 0);
+                u3a4 mm;
+                mm.x = m.x; mm.y = m.y; mm.z = m.z;
+                bcast_jrow(mm, rj);
+            }
 #endif
             const uint32_t* ld = lD0 + buf * LBUF;
             const uint32_t* lc = lC0 + buf * LBUF;
