@@ -27,6 +27,8 @@ struct DevBuf {
 struct mdx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t aux = nullptr;               // LK class / A kernels run ahead here (MDX_LK_AUX=0: off)
+    hipEvent_t lkev[kMaxLevels + 1] = {};
     mdx_params prm{};
     int max_w = 0, max_h = 0, max_batch = 0;
     DevBuf pyr1, pyr2, der, fits;            // pyramid / derivative / fit workspace
@@ -37,6 +39,7 @@ struct mdx_ctx {
     DevBuf csum;                             // classify: per-block summaries
     bool lk_debug = false;
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
+    int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
     int plan_w = -1, plan_h = -1, plan_ps = -1, plan_ml = -1;
     ClassPlan plan{};
     bool timing = false;
@@ -152,8 +155,8 @@ static int ensure_workspace(mdx_ctx* c, const Geometry& g, int batch)
 
 // Residue classes of the grid at each level (see mdx_lk.hip), the class-grouped point order and
 // the class-plane layout.  Rebuilt and uploaded only when frame size / pixel_step / levels change.
-// plan.nch == 0 means the 8-point union of some group is wider than 512 columns (pixel_step >~ 66):
-// the caller then runs the single-kernel LK instead.
+// plan.nch == 0 means some group's union is wider than 512 columns (pixel_step >~ 66) or a pair's
+// class slab exceeds 2 GB: the caller then runs the single-kernel LK instead.
 static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps, int batch)
 {
     int rc;
@@ -165,7 +168,7 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
         int16_t* cmap = tab.data();
         int16_t* rlist = tab.data() + kMaxLevels * 2 * 128;
         ClassPlan P{};
-        int umax = 0;
+        bool usable = true;
         for (int l = 0; l < g.nlev; l++) {
             const int m = (1 << l) - 1;
             int n[2] = {0, 0};
@@ -185,40 +188,57 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
             ClassLevel& C = P.lv[l];
             C.nrx = n[0];
             C.nry = n[1];
-            // columns: each class's members in x order, the run padded to a multiple of 8 (-1)
+            // columns: each class's members in x order.  Group size per level: 4 points when a
+            // 4-group's union fits 64 columns (no extra union loads), else 8 (MDX_LK_G forces one)
             C.ord_off = (int)ord.size();
             const int16_t* cmx = cmap + (l * 2 + 0) * 128;
             const float scale = (float)(1. / (1 << l));
             auto ipx_of = [&](int gx) { return (int)std::floor((float)(gx * ps) * scale - 19.5f); };
-            for (int cls = 0; cls < n[0]; cls++) {
-                const size_t run0 = ord.size();
-                for (int i = 0; i < nx; i++)
-                    if (cmx[(i * ps) & m] == cls) ord.push_back((int16_t)i);
-                for (size_t q = run0; q < ord.size(); q += 8) {    // union width of each 8-group
-                    const size_t last = std::min(ord.size(), q + 8) - 1;
-                    umax = std::max(umax, ipx_of(ord[last]) - ipx_of(ord[q]) + kWin);
-                }
-                while ((ord.size() - run0) % 8) ord.push_back((int16_t)-1);
+            std::vector<std::vector<int16_t>> runs(n[0]);
+            for (int i = 0; i < nx; i++) runs[cmx[(i * ps) & m]].push_back((int16_t)i);
+            auto union_of = [&](int G) {
+                int u = 0;
+                for (const auto& r : runs)
+                    for (size_t q = 0; q < r.size(); q += G)
+                        u = std::max(u, ipx_of(r[std::min(r.size(), q + G) - 1]) - ipx_of(r[q]) + kWin);
+                return u;
+            };
+            const int u4 = union_of(4), u8 = union_of(8);
+            if (c->lk_g == 4) {
+                C.G = 4;
+                C.UW = u4 <= 64 ? 64 : u4 <= 128 ? 128 : 0;
+            } else if (c->lk_g != 8 && u4 <= 64) {
+                C.G = 4;
+                C.UW = 64;
+            } else {
+                C.G = 8;
+                C.UW = u8 <= 128 ? 128 : u8 <= 256 ? 256 : u8 <= 512 ? 512 : 0;
+            }
+            if (C.UW == 0) usable = false;
+            for (const auto& r : runs) {   // each run padded to a multiple of G with -1
+                ord.insert(ord.end(), r.begin(), r.end());
+                for (size_t q = r.size(); q % C.G; q++) ord.push_back((int16_t)-1);
             }
             C.nxp = (int)ord.size() - C.ord_off;
-            // rows: grouped by class the same way (no padding: a wave takes one row)
+            // rows: grouped by class the same way (no padding: a group is one row)
             const size_t r0 = ord.size();
             for (int i = 0; i < ny; i++) ord.push_back((int16_t)i);
             const int16_t* cmy = cmap + (l * 2 + 1) * 128;
             std::stable_sort(ord.begin() + r0, ord.end(),
                              [&](int16_t u, int16_t v) { return cmy[(u * ps) & m] < cmy[(v * ps) & m]; });
         }
-        P.nch = umax <= 128 ? 1 : umax <= 256 ? 2 : umax <= 512 ? 4 : 0;
-        const int UW = 128 * std::max(P.nch, 1);
         long long off = 0;
         for (int l = 0; l < g.nlev; l++) {
             ClassLevel& C = P.lv[l];
             C.UH = g.lv[l].h + 79;
-            C.PW = (g.lv[l].w + kPad + UW + 3) & ~3;
+            C.PW = (g.lv[l].w + kPad + std::max(C.UW, 64) + 3) & ~3;
             C.class_bytes = (long long)C.UH * C.PW * 8;
             C.off = off;
             off += (long long)C.nrx * C.nry * C.class_bytes;
         }
+        // the kernels address a pair's slab with 32-bit buffer offsets
+        if (off > 0x7fff0000LL) usable = false;
+        P.nch = usable ? 1 : 0;
         P.bytes_per_pair = (off + 255) / 256 * 256;
         tab.insert(tab.end(), ord.begin(), ord.end());
         if ((rc = ensure(c, c->ctab, tab.size() * sizeof(int16_t))) != MDX_OK) return rc;
@@ -256,11 +276,23 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     c->max_h = max_h;
     c->max_batch = max_batch;
     if (const char* e = std::getenv("MDX_LK_IMPL")) c->lk_impl = std::atoi(e) == 1 ? 1 : 2;
+    if (const char* e = std::getenv("MDX_LK_G")) c->lk_g = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         g_create_err = "hipStreamCreate failed";
         delete c;
         return nullptr;
+    }
+    const char* ea = std::getenv("MDX_LK_AUX");
+    if (!ea || std::atoi(ea) != 0) {
+        bool ok = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; ok && i <= kMaxLevels; i++)
+            ok = hipEventCreateWithFlags(&c->lkev[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            g_create_err = "aux stream / event creation failed";
+            mdx_destroy(c);
+            return nullptr;
+        }
     }
     Geometry g = make_geometry(max_w, max_h, prm.max_level);
     if (ensure_workspace(c, g, max_batch) != MDX_OK) {
@@ -286,6 +318,9 @@ extern "C" int mdx_destroy(mdx_ctx* c)
         delete[] c->ev;
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
+    for (hipEvent_t e : c->lkev)
+        if (e) (void)hipEventDestroy(e);
     delete c;
     return MDX_OK;
 }
@@ -436,7 +471,10 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
                 const char* e = std::getenv("MDX_LK_DEBUG_PT");
                 a.dbg_pt = e ? std::atoi(e) : -1;
             }
-            HIP_OR_RETURN(c, launch_lk_v2(s, batch, a, c->cls.as<uint8_t>()));
+            const size_t abytes = (size_t)g.nlev * batch * npts * sizeof(float4);
+            if ((rc = ensure(c, c->Abuf, abytes + (size_t)batch * kMaxLevels * 8 * sizeof(int))) != MDX_OK) return rc;
+            HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
+                                          reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes)));
         }
     }
     mark(c, 4);

@@ -48,14 +48,16 @@ struct ClassLevel {
     int UH, PW;              // plane rows (h + 79), plane width in elements (multiple of 4)
     long long off;           // byte offset of this level inside a pair's class slab
     long long class_bytes;   // UH * PW * 8
-    int nxp;                 // length of the padded class-grouped column order (multiple of 8)
+    int nxp;                 // length of the padded class-grouped column order (multiple of G)
     int ord_off;             // offset of this level's order tables in LkArgs::ord
+    int G;                   // points per LK group (4 or 8)
+    int UW;                  // union columns per group (64, 128, 256 or 512)
 };
 
 struct ClassPlan {
     ClassLevel lv[kMaxLevels];
     long long bytes_per_pair;
-    int nch;                 // union chunks of 128 columns per 8-point group (1, 2 or 4)
+    int nch;                 // 0: some group's union is wider than 512 columns (single-kernel LK)
 };
 
 struct LkClassArgs {
@@ -93,7 +95,11 @@ hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const u
 hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level);
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level);
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
-hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint8_t* cls);
+// Ab: [nlev][batch][npts] per-point (A11, A12, A22, 1/D); qctr: [batch][kMaxLevels][8] queue
+// heads.  aux (may be null): second stream for the flow-independent class / A kernels; ev: kMaxLevels
+// + 1 events (no timing) used to order the two streams.
+hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
+                        float4* Ab, int* qctr);
 hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
                                int ny, int pixel_step, double min_vector_size, double* vectors, PairFit* fits,
                                int fit_mode, const double* H_external, void* scratch);

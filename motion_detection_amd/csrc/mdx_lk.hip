@@ -1,9 +1,9 @@
 // mdx_lk.hip -- pyramidal Lucas-Kanade (reference row A5: calcOpticalFlowPyrLK as called at
 // optical_flow_calculator.cpp:71), restructured for CDNA4 while keeping OpenCV 2.4's x86 SSE2
 // arithmetic bit for bit.  This is the "class plane" LK (MDX_LK_IMPL=2, default); the
-// single-kernel k_lk in mdx_kernels.hip is the general fallback.
+// single-kernel k_lk in mdx_kernels.hip is the fallback for very sparse grids.
 //
-// Per pyramid level, from maxLevel down to 0, two kernels:
+// Per pyramid level, from maxLevel down to 0, three kernels:
 //
 //  k_lk_class  The interpolated window values (I*32 descaled by 9 bits, Ix/Iy descaled by 14
 //              bits) over the whole padded level, once per fractional-offset class.  At level L a
@@ -12,21 +12,25 @@
 //              16x-overlapping per-window interpolation of the reference becomes one
 //              interpolation per class and pixel.  Natural row-major layout, two arrays per
 //              class: D = (Ix | Iy << 16) and C = 256 - 512*I (the J-chain bias, see below).
-//  k_lk_level  Per point: the gradient matrix sums A11/A12/A22 over the window, the minEig /
-//              determinant tests, then the Newton iterations.
+//  k_lk_A      Per point: the gradient matrix sums A11/A12/A22 over the window and the minEig /
+//              determinant tests.
+//  k_lk_iter   The Newton iterations, on persistent waves fed from per-XCD work queues.
 //
-// Work mapping of k_lk_level.  A wave = 16 points x 4 lanes: lane k of a point owns SSE lane k
-// (window columns x = 4g + k, g = 0..9, rows in order) and keeps its partial sums in registers;
-// partials are combined across the lane quad in the reference's order (A: ((P0+P1)+P2)+P3,
-// b: (P0+P2)+(P1+P3)).  The 16 points of a wave are two groups of 8 consecutive members of one
-// residue class along one grid row (host-built class-grouped order, runs padded to 8), so a
-// group's windows share their rows and overlap in columns: per window row the group needs one
-// contiguous "union" segment of <= 128*NCH columns of D and C.  Each half-wave loads its
-// group's segment with one coalesced dwordx4 per array and lane, stores it to a double-buffered
-// LDS row, and every lane then reads its 10 chain elements with ds_read_b32.  That replaces the
-// 6 scattered dwordx2/x4 loads per lane and row that bound the previous design on the texture
-// data path (TD busy 97%, VALU 38%).  J (the moving window in the next frame) differs per point:
-// its row segment is loaded once per lane quad (3 dwords per lane) and shared by DPP.
+// The first two depend on the previous frame only, so they run ahead on an auxiliary stream
+// (level L-1's class planes and A sums while level L iterates) and fill the iteration kernel's
+// tail; every level keeps its own planes, A buffer and queue heads.
+//
+// Work mapping.  Lane k of a point owns SSE lane k (window columns x = 4g + k, g = 0..9, rows in
+// order) and keeps its partial sums in registers; partials are combined across the lane quad in
+// the reference's order (A: ((P0+P1)+P2)+P3, b: (P0+P2)+(P1+P3)).  Points are processed in
+// groups of G (4 or 8) consecutive members of one residue class along one grid row (host-built
+// class-grouped order, runs padded to G), so a group's windows share their rows and overlap in
+// columns: per window row the group needs one contiguous "union" segment of UW columns of D
+// and C.  The group's lanes load it with coalesced dwordx4, store it to a double-buffered LDS
+// row, and every lane then reads its 10 chain elements from LDS.  That replaces the 6 scattered
+// dwordx2/x4 loads per lane and row that bound a per-point design on the texture data path (TD
+// busy 97%, VALU 38%).  J (the moving window in the next frame) differs per point: its row
+// segment is loaded once per lane quad (3 dwords per lane) and shared by DPP.
 //
 // Arithmetic: J taps via v_perm_b32 + v_dot2_i32_i16 (signed weights: w11 may be -1);
 // dot2(pa, W0, dot2(pb, W1, C)) >> 9 == ((S + 256) >> 9) - I exactly, because C = 256 - 512*I
@@ -36,6 +40,9 @@
 #include "mdx_internal.h"
 
 #include <float.h>
+
+#include <algorithm>
+#include <cstdlib>
 
 namespace mdx {
 
@@ -201,171 +208,295 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
 }
 
 // ------------------------------------------------------------------ one pyramid level
-// grid: x -> wave (16 points), y -> pair (XCD-remapped as one linear range).  Levels run as
-// separate launches from maxLevel down to 0; the position carried between them is next_pts
-// (the reference's nextPts[ptidx], stored every level).
-template <int NCH>
-#ifdef LKX_WPE   // timing variants: occupancy request
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE, 8)))
-#else
-__global__ __launch_bounds__(64)
-#endif
-void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
-{
-    constexpr int UW = NCH * 128;           // union columns per group
-    constexpr float HALFW = 19.5f;
-    constexpr float FLT_SCALE = 1.f / (1 << 20);
-    // [buf][group][D, C][UW]: a window row's union segment, double-buffered across rows
-    __shared__ __attribute__((aligned(16))) uint32_t lds[2][2][2][UW];
+// Work units.  A GROUP is G consecutive members of one residue class along one grid row (host
+// order: each class's run padded to a multiple of G with -1).  A SLOT is the 4G lanes holding one
+// group, a lane quad per point.  Per window row a slot needs one contiguous "union" segment of UW
+// plane columns of D (and C): NL coalesced dwordx4 per lane, staged in a double-buffered LDS row.
+//
+// Per level two kernels follow k_lk_class:
+//  k_lk_A     static groups (one slot each): the gradient sums A11/A12/A22 and the minEig /
+//             determinant tests, stored per point as (A11, A12, A22, 1/D) -- 1/D = 0 marks a point
+//             the reference skips at this level.
+//  k_lk_iter  the Newton iterations.  Points iterate 1..max_iters times; a slot whose G points
+//             iterate in lockstep costs the max over the group, and a static wave the max over
+//             all its groups.  So the waves are persistent and each slot, when its group retires,
+//             takes the next group from a per-(level, pair) atomic counter: slots of one wave
+//             run out of step, only the group-internal lockstep remains.
+template <int G, int UW>
+struct LkShape {
+    static constexpr int LPS = 4 * G;            // lanes per slot
+    static constexpr int S = 64 / LPS;           // slots per wave
+    static constexpr int NL = UW / (4 * LPS);    // dwordx4 per lane and union row
+    static constexpr int SPAD = 0;               // LDS words per slot row beyond the union
+    static_assert(NL >= 1 && NL * 4 * LPS == UW, "union width must be a multiple of a slot's row load");
+};
 
-    const int lane = threadIdx.x, k = lane & 3, grp = lane >> 5, gl = lane & 31;
+struct GroupGeom {
+    int gx, gy;       // grid point of this lane quad
+    bool valid;       // the quad holds a real point (not run padding / no group)
+    int ipx, ipy;     // floor of the window origin at this level
+    int off;          // the point's first column inside the union
+    int v0;           // first window row in the class plane
+    uint32_t dlane;   // byte offset in the pair's class slab of this lane's union chunk, row 0
+};
+
+// geometry of group g (-1 = none) for lane sl of its slot
+template <int G, int UW>
+__device__ __forceinline__ GroupGeom group_geom(const LkArgs& a, const ClassLevel& C, int level, int g, int sl)
+{
+    GroupGeom r;
+    const int16_t* xo = a.ord + C.ord_off;
+    const int16_t* yo = xo + C.nxp;
+    const bool has = g >= 0;
+    const int gg = has ? g : 0;
+    const int cg = gg / a.ny, row = gg - cg * a.ny;   // column-group major: neighbours share rows
+    const int e0 = cg * G;
+    const int gxv = has ? xo[e0 + (sl >> 2)] : -1;
+    r.valid = gxv >= 0;
+    r.gx = r.valid ? gxv : 0;
+    r.gy = yo[row];
+    const float scale = (float)(1. / (1 << level));
+    r.ipx = (int)floorf((float)(r.gx * a.pixel_step) * scale - 19.5f);
+    r.ipy = (int)floorf((float)(r.gy * a.pixel_step) * scale - 19.5f);
+    // a group's first entry is a real point (runs start at multiples of G, padding at their ends)
+    // and its leftmost one (runs sorted by x)
+    const int gx0 = has ? xo[e0] : 0;
+    const int ipx0 = (int)floorf((float)(gx0 * a.pixel_step) * scale - 19.5f);
+    const int m = (1 << level) - 1;
+    const int cx = class_of(a.cmap, level, 0, (gx0 * a.pixel_step) & m);
+    const int cy = class_of(a.cmap, level, 1, (r.gy * a.pixel_step) & m);
+    const int ub = min(max(ipx0 + kPad, 0), C.PW - UW);            // union start column
+    r.off = min(max(r.ipx + kPad - ub, 0), UW - kWin);
+    r.v0 = min(max(r.ipy + kPad, 0), C.UH - kWin);
+    r.dlane = (uint32_t)(C.off + (long long)(cy * C.nrx + cx) * C.class_bytes) + 4u * (uint32_t)(ub + 4 * sl);
+    return r;
+}
+
+// ---- A pass.  grid: x -> wave (S static groups), y -> pair (XCD-remapped as one range)
+template <int G, int UW>
+__global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict__ cls, float4* __restrict__ Ab,
+                                             int* __restrict__ qctr, int level, int ngroups)
+{
+    using Sh = LkShape<G, UW>;
+    constexpr int LPS = Sh::LPS, S = Sh::S, NL = Sh::NL;
+    constexpr float FLT_SCALE = 1.f / (1 << 20);
+    constexpr int SW = UW + Sh::SPAD;                             // words per slot row
+    __shared__ __attribute__((aligned(16))) uint32_t lds[2][S][SW];
+
+    const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
     const int nw = gridDim.x;
     const int bid = xcd_remap(blockIdx.x + nw * blockIdx.y, nw * gridDim.y);
     const int pair = bid / nw, w = bid % nw;
+    if (bid == 0 && lane < 8) qctr[level * 8 + lane] = 0;          // k_lk_iter's queue heads
     const ClassLevel& C = a.plan.lv[level];
     const Level L = a.g.lv[level];
-    const int16_t* xo = a.ord + C.ord_off;
-    const int16_t* yo = xo + C.nxp;
-    const int slot = (w / a.ny) * 16 + (lane >> 2);
-    const int gxv = slot < C.nxp ? xo[slot] : -1;
-    const bool valid = gxv >= 0;
-    const int gx = valid ? gxv : 0, gy = yo[w % a.ny];
-    const int pt = gx * a.ny + gy;
-    const long long po = (long long)pair * a.npts + pt;
+    const int g = w * S + slot;
+    const GroupGeom q = group_geom<G, UW>(a, C, level, g < ngroups ? g : -1, sl);
+    bool ok = q.valid && !(q.ipx < -kWin || q.ipx >= L.w || q.ipy < -kWin || q.ipy >= L.h);
 
-    const float scale = (float)(1. / (1 << level));
-    const float px0 = (float)(gx * a.pixel_step), py0 = (float)(gy * a.pixel_step);
-    const float ppx = px0 * scale - HALFW, ppy = py0 * scale - HALFW;
-    const int ipx = (int)floorf(ppx), ipy = (int)floorf(ppy);
-    bool ok = valid && !(ipx < -kWin || ipx >= L.w || ipy < -kWin || ipy >= L.h);
-
-    // group (8 points) geometry: its first slot holds its leftmost point (runs sorted by x)
-    const int slot0 = (w / a.ny) * 16 + grp * 8;
-    const int gx0v = slot0 < C.nxp ? xo[slot0] : -1;
-    const int gx0 = gx0v >= 0 ? gx0v : 0;
-    const int ipx0 = (int)floorf((float)(gx0 * a.pixel_step) * scale - HALFW);
-    const int m = (1 << level) - 1;
-    const int cx = class_of(a.cmap, level, 0, (gx0 * a.pixel_step) & m);
-    const int cy = class_of(a.cmap, level, 1, (gy * a.pixel_step) & m);
-    const uint8_t* cbase = cls + (long long)pair * a.plan.bytes_per_pair + C.off +
-                           (long long)(cy * C.nrx + cx) * C.class_bytes;
-    const int ub = min(max(ipx0 + kPad, 0), C.PW - UW);          // union start column
-    const int off = min(max(ipx + kPad - ub, 0), UW - kWin);     // this point's column in it
-    const uint32_t* gD = reinterpret_cast<const uint32_t*>(cbase) + ub + 4 * gl;
-    [[maybe_unused]] const uint32_t* gC = gD + (long long)C.UH * C.PW;
-    // buffer addressing: descriptor over this pair's class slab, 32-bit lane offsets; the C
-    // array sits a constant UH*PW*4 bytes after D (scalar offset field)
-    const uint8_t* cslab = cls + (long long)pair * a.plan.bytes_per_pair;
-    const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cslab, a.plan.bytes_per_pair);
-    const uint32_t dlane = (uint32_t)(reinterpret_cast<const uint8_t*>(gD) - cslab);
-    const int csoff = C.UH * C.PW * 4;
+    const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cls + (long long)pair * a.plan.bytes_per_pair, a.plan.bytes_per_pair);
     const uint32_t rowb = (uint32_t)C.PW * 4;
-    const int v0 = min(max(ipy + kPad, 0), C.UH - kWin);          // first window row (wave-uniform)
-    const uint32_t* lD0 = &lds[0][grp][0][off + k];
-    const uint32_t* lC0 = &lds[0][grp][1][off + k];
-    constexpr int LBUF = 2 * 2 * UW;                              // words per buffer
-
-    float npx, npy;
-    if (level == a.maxl) {
-        npx = px0 * scale;
-        npy = py0 * scale;
-    } else {
-        const float2 q = valid ? reinterpret_cast<const float2*>(a.next_pts)[po] : make_float2(0.f, 0.f);
-        npx = q.x * 2.f;
-        npy = q.y * 2.f;
-    }
-    int status = 1;
-    if (valid && !ok && level == 0) status = 0;
-
-    uint4 rd[NCH], rc[NCH];
-    auto gload = [&](int v, bool withC) {
+    uint32_t roff = q.dlane + (uint32_t)q.v0 * rowb;
+    const uint32_t* lD0 = &lds[0][slot][q.off + k];
+    // rows are loaded PF ahead (this kernel has few waves' worth of VALU work to hide latency)
+    constexpr int PF = 4;
+    uint4 rq[PF][NL];
+    auto gload = [&](uint4 (&rd)[NL]) {
 #pragma unroll
-        for (int c = 0; c < NCH; c++) {
-#ifdef LKX_NOBUF
-            const u4a4 t = *reinterpret_cast<const u4a4*>(gD + (long long)v * C.PW + 128 * c);
+        for (int c = 0; c < NL; c++) {
+            const v4u t = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)(roff + 16u * LPS * c), 0, 0);
             rd[c] = make_uint4(t.x, t.y, t.z, t.w);
-            if (withC) {
-                const u4a4 s = *reinterpret_cast<const u4a4*>(gC + (long long)v * C.PW + 128 * c);
-                rc[c] = make_uint4(s.x, s.y, s.z, s.w);
-            }
-#else
-            const uint32_t vo = dlane + (uint32_t)v * rowb + 512u * c;
-            const v4u t = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)vo, 0, 0);
-            rd[c] = make_uint4(t.x, t.y, t.z, t.w);
-            if (withC) {
-                const v4u q = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)vo, csoff, 0);
-                rc[c] = make_uint4(q.x, q.y, q.z, q.w);
-            }
-#endif
         }
+        roff += rowb;
     };
-    auto lstore = [&](int buf, bool withC) {
+    auto lstore = [&](int buf, const uint4 (&rd)[NL]) {
 #pragma unroll
-        for (int c = 0; c < NCH; c++) {
-            *reinterpret_cast<uint4*>(&lds[buf][grp][0][128 * c + 4 * gl]) = rd[c];
-            if (withC) *reinterpret_cast<uint4*>(&lds[buf][grp][1][128 * c + 4 * gl]) = rc[c];
-        }
+        for (int c = 0; c < NL; c++) *reinterpret_cast<uint4*>(&lds[buf][slot][4 * LPS * c + 4 * sl]) = rd[c];
     };
 
-    // ---- A sums: lane k owns SSE lane k (columns 4g+k), rows in order; ((P0+P1)+P2)+P3
-    float A11, A12, A22;
+    // lane k owns SSE lane k (columns 4g+k), rows in order; ((P0+P1)+P2)+P3 across the quad
+    f2 sd = {0.f, 0.f};
+    float s12 = 0.f;
     {
-        f2 sd = {0.f, 0.f};
-        float s12 = 0.f;
-        gload(v0, false);
-        lstore(0, false);
-        wave_lds_fence();
-#pragma unroll 2
-        for (int y = 0; y < kWin; y++) {
-            const int buf = y & 1;
-            if (y + 1 < kWin) gload(v0 + y + 1, false);
-            const uint32_t* ld = lD0 + buf * LBUF;
+        uint4 r0[NL];
+        gload(r0);
 #pragma unroll
-            for (int g = 0; g < 10; g++) {
-                const uint32_t d = ld[4 * g];
-                const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
-                sd = sd + f * f;                 // (Ix*Ix, Iy*Iy)
-                s12 = s12 + f.x * f.y;           // Ix*Iy
-            }
-            if (y + 1 < kWin) lstore(buf ^ 1, false);
-            wave_lds_fence();
-        }
-        const float a11 = ((quad_bcast<0>(sd.x) + quad_bcast<1>(sd.x)) + quad_bcast<2>(sd.x)) + quad_bcast<3>(sd.x);
-        const float a12 = ((quad_bcast<0>(s12) + quad_bcast<1>(s12)) + quad_bcast<2>(s12)) + quad_bcast<3>(s12);
-        const float a22 = ((quad_bcast<0>(sd.y) + quad_bcast<1>(sd.y)) + quad_bcast<2>(sd.y)) + quad_bcast<3>(sd.y);
-        A11 = a11 * FLT_SCALE;
-        A12 = a12 * FLT_SCALE;
-        A22 = a22 * FLT_SCALE;
+        for (int i = 0; i < PF; i++) gload(rq[i]);
+        lstore(0, r0);
     }
+    wave_lds_fence();
+#pragma unroll
+    for (int y = 0; y < kWin; y++) {
+        const int buf = y & 1;
+        const uint32_t* ld = lD0 + buf * (S * SW);
+#pragma unroll
+        for (int gi = 0; gi < 10; gi++) {
+            const uint32_t d = ld[4 * gi];
+            const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
+            sd = sd + f * f;                 // (Ix*Ix, Iy*Iy)
+            s12 = s12 + f.x * f.y;           // Ix*Iy
+        }
+        if (y + 1 < kWin) {
+            lstore(buf ^ 1, rq[y % PF]);     // row y+1
+            if (y + 1 + PF < kWin) gload(rq[y % PF]);
+        }
+        wave_lds_fence();
+    }
+    const float a11 = ((quad_bcast<0>(sd.x) + quad_bcast<1>(sd.x)) + quad_bcast<2>(sd.x)) + quad_bcast<3>(sd.x);
+    const float a12 = ((quad_bcast<0>(s12) + quad_bcast<1>(s12)) + quad_bcast<2>(s12)) + quad_bcast<3>(s12);
+    const float a22 = ((quad_bcast<0>(sd.y) + quad_bcast<1>(sd.y)) + quad_bcast<2>(sd.y)) + quad_bcast<3>(sd.y);
+    const float A11 = a11 * FLT_SCALE, A12 = a12 * FLT_SCALE, A22 = a22 * FLT_SCALE;
     float Dinv = 0.f;
     if (ok) {
         const float D = A11 * A22 - A12 * A12;
         const float minEig = (A22 + A11 - __builtin_sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
                              (float)(2 * kWin * kWin);
-        if (minEig < a.min_eig || D < FLT_EPSILON) {
-            ok = false;
-            if (level == 0) status = 0;
-        } else {
-            Dinv = 1.f / D;
-        }
+        if (!(minEig < a.min_eig || D < FLT_EPSILON)) Dinv = 1.f / D;
     }
+    if (q.valid && k == 0) Ab[(long long)pair * a.npts + q.gx * a.ny + q.gy] = make_float4(A11, A12, A22, Dinv);
+}
 
-    // ---- Newton iterations
+// ---- Newton iterations.  grid: x -> persistent wave (a multiple of 8).  The level's work list
+// is every pair's groups, pair-major; it is cut into 8 contiguous ranges, one per XCD (blocks are
+// dealt to the XCDs round-robin), each with its own queue head.  An XCD's waves thus work on
+// neighbouring groups of one pair at a time, whose class-plane rows its L2 holds -- per-pair
+// queues spread every XCD over several pairs at once and doubled the L2 misses.  Levels run as
+// separate launches from maxLevel down to 0; the position carried between them is next_pts (the
+// reference's nextPts[ptidx], stored every level).
+template <int G, int UW>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_lk_iter(
+    LkArgs a, const uint8_t* __restrict__ cls, const float4* __restrict__ Ab, int* __restrict__ qctr, int level,
+    int ngroups, int batch)
+{
+    using Sh = LkShape<G, UW>;
+    constexpr int LPS = Sh::LPS, S = Sh::S, NL = Sh::NL;
+    constexpr float HALFW = 19.5f;
+    constexpr float FLT_SCALE = 1.f / (1 << 20);
+    constexpr int SW = 2 * UW + Sh::SPAD;                         // words per slot: D row, C row, pad
+    constexpr int LBUF = S * SW;                                  // words per LDS buffer
+    __shared__ __attribute__((aligned(16))) uint32_t lds[2][S][SW];
+
+    const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
+    const unsigned long long smask = ((1ull << LPS) - 1) << (slot * LPS);
+    const int xcd = blockIdx.x & 7;
+    const long long T = (long long)batch * ngroups;
+    const long long cb = T * xcd / 8, ce = T * (xcd + 1) / 8;     // this XCD's range of the work list
+    const int p0 = (int)(cb / ngroups);
+    const int np = ce > cb ? (int)((ce - 1) / ngroups) - p0 + 1 : 1;
+    int* ctr = qctr + level * 8 + xcd;
+    const ClassLevel& C = a.plan.lv[level];
+    const Level L = a.g.lv[level];
+    // buffer addressing: descriptors over the range's class slabs and next-frame pyramids (the
+    // host keeps them below 2 GB), 32-bit lane offsets; the C array sits a constant UH*PW*4 bytes
+    // after D (scalar offset field)
+    const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cls + (long long)p0 * a.plan.bytes_per_pair, np * a.plan.bytes_per_pair);
+    const int csoff = C.UH * C.PW * 4;
+    const uint32_t rowb = (uint32_t)C.PW * 4;
     const int pitch = L.pitch;
-    const uint8_t* Jb = a.pyr2 + (long long)pair * a.g.img_bytes + L.img_off + L.core();
-    const __amdgpu_buffer_rsrc_t jrs = buf_rsrc(a.pyr2 + (long long)pair * a.g.img_bytes, a.g.img_bytes);
+    const __amdgpu_buffer_rsrc_t jrs = buf_rsrc(a.pyr2 + (long long)p0 * a.g.img_bytes, np * a.g.img_bytes);
     const uint32_t jbase = (uint32_t)(L.img_off + L.core());
-    float nx = npx - HALFW, ny = npy - HALFW;
-    float pdx = 0.f, pdy = 0.f;
-    bool act = ok;
-    int iters = 0;
-    for (int j = 0; j < a.max_iters; j++) {
-        if (!__any(act)) break;
+    const float scale = (float)(1. / (1 << level));
+
+    // slot state (uniform over the slot's lanes)
+    bool live = false, dead = false;
+    int j = 0;
+    // point state
+    GroupGeom q{};
+    int pt = 0, pair = 0;
+    long long po = 0;
+    uint32_t jrel = 0;                                            // pair's pyramid in jrs
+    float A11 = 0.f, A12 = 0.f, A22 = 0.f, Dinv = 0.f;
+    float nx = 0.f, ny = 0.f, npx = 0.f, npy = 0.f, pdx = 0.f, pdy = 0.f;
+    bool act = false;
+    int status = 1, iters = 0;
+
+    auto retire = [&]() {
+        if (level == 0 && q.valid && status) {
+            const int fx = (int)floorf(npx - HALFW), fy = (int)floorf(npy - HALFW);
+            if (fx < -kWin || fx >= L.w || fy < -kWin || fy >= L.h) status = 0;
+        }
+        if (q.valid && k == 0) {
+            if (a.dbg)
+                a.dbg[((long long)pair * a.g.nlev + level) * a.npts + pt] = make_float4(npx, npy, (float)iters, (float)status);
+            reinterpret_cast<float2*>(a.next_pts)[po] = make_float2(npx, npy);
+            if (level == 0) a.status[po] = (uint8_t)status;
+        }
+    };
+
+    uint4 rd[NL], rc[NL];
+    uint32_t roff = 0;
+    auto gload = [&]() {
+#pragma unroll
+        for (int c = 0; c < NL; c++) {
+            const int vo = (int)(roff + 16u * LPS * c);
+            const v4u t = __builtin_amdgcn_raw_buffer_load_b128(crs, vo, 0, 0);
+            rd[c] = make_uint4(t.x, t.y, t.z, t.w);
+            const v4u u = __builtin_amdgcn_raw_buffer_load_b128(crs, vo, csoff, 0);
+            rc[c] = make_uint4(u.x, u.y, u.z, u.w);
+        }
+        roff += rowb;
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int c = 0; c < NL; c++) {
+            *reinterpret_cast<uint4*>(&lds[buf][slot][4 * LPS * c + 4 * sl]) = rd[c];
+            *reinterpret_cast<uint4*>(&lds[buf][slot][UW + 4 * LPS * c + 4 * sl]) = rc[c];
+        }
+    };
+
+    for (;;) {
+        // ---- refill: each slot without a live group takes the next one; a group with no point
+        // left to iterate retires at once
+        for (;;) {
+            const bool need = !live && !dead;
+            if (!__any(need)) break;
+            if (need) {
+                int gi = 0;
+                if (sl == 0) gi = atomicAdd(ctr, 1);
+                gi = __shfl(gi, slot * LPS);
+                if (cb + gi >= ce) {
+                    dead = true;
+                } else {
+                    const long long gl = cb + gi;
+                    pair = (int)(gl / ngroups);
+                    q = group_geom<G, UW>(a, C, level, (int)(gl - (long long)pair * ngroups), sl);
+                    q.dlane += (uint32_t)((long long)(pair - p0) * a.plan.bytes_per_pair);
+                    jrel = (uint32_t)((long long)(pair - p0) * a.g.img_bytes);
+                    pt = q.gx * a.ny + q.gy;
+                    po = (long long)pair * a.npts + pt;
+                    const float4 Av = q.valid ? Ab[po] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    A11 = Av.x;
+                    A12 = Av.y;
+                    A22 = Av.z;
+                    Dinv = Av.w;
+                    if (level == a.maxl) {
+                        npx = (float)(q.gx * a.pixel_step) * scale;
+                        npy = (float)(q.gy * a.pixel_step) * scale;
+                    } else {
+                        const float2 p = q.valid ? reinterpret_cast<const float2*>(a.next_pts)[po] : make_float2(0.f, 0.f);
+                        npx = p.x * 2.f;
+                        npy = p.y * 2.f;
+                    }
+                    act = Dinv > 0.f;   // real point, window inside, eigenvalue / determinant tests passed
+                    status = (level == 0 && q.valid && !act) ? 0 : 1;
+                    nx = npx - HALFW;
+                    ny = npy - HALFW;
+                    pdx = 0.f;
+                    pdy = 0.f;
+                    iters = 0;
+                    j = 0;
+                    live = (__ballot(act) & smask) != 0 && a.max_iters > 0;
+                    if (!live) retire();
+                }
+            }
+        }
+        if (!__any(live)) break;
+
+        // ---- one Newton iteration of every live group.  Lanes that are not iterating (or fail
+        // the bounds test) run the row loop on a safe address and drop the result, so the loop
+        // is wave-uniform (it also carries every slot's LDS staging).
         f2 acc = {0.f, 0.f};
         if (act) iters++;
-        // Position, bounds and weights; lanes that are not iterating (or fail the bounds
-        // test) run the row loop on a safe address and drop the result, so the loop below is
-        // wave-uniform (it also carries the group's LDS staging).
         int inx = (int)floorf(nx), iny = (int)floorf(ny);
         if (act && (inx < -kWin || inx >= L.w || iny < -kWin || iny >= L.h)) {
             act = false;
@@ -380,39 +511,29 @@ void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
         const s2 W1 = {(short)v10, (short)v11};
         const int o = (inx & 3) + k;
         const unsigned sel = (unsigned)o | 0x0c00u | ((unsigned)(o + 1) << 16) | 0x0c000000u;
-        const uint32_t* jrow = reinterpret_cast<const uint32_t*>(Jb + (long long)iny * pitch + (inx & ~3));
-        [[maybe_unused]] const int jstride = pitch >> 2;
-        uint32_t joff = jbase + (uint32_t)(iny * pitch + (inx & ~3) + 12 * k);   // buffer offset of this lane's J dwords
+        uint32_t joff = jrel + jbase + (uint32_t)(iny * pitch + (inx & ~3) + 12 * k);   // this lane's J dwords
         // taps of the current window row (pa) are the previous row's lower taps (pb)
         s2 pa[10], pb[10];
         {
+            const v3u m = __builtin_amdgcn_raw_buffer_load_b96(jrs, (int)joff, 0, 0);
+            u3a4 mm;
+            mm.x = m.x; mm.y = m.y; mm.z = m.z;
             uint32_t rj[11];
-            load_jrow_quad(jrow, k, rj);
+            bcast_jrow(mm, rj);
 #pragma unroll
-            for (int g = 0; g < 10; g++) pa[g] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[g + 1], rj[g], sel));
+            for (int gi = 0; gi < 10; gi++) pa[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
         }
-        gload(v0, true);
-        lstore(0, true);
+        roff = q.dlane + (uint32_t)q.v0 * rowb;
+        const uint32_t* lD0 = &lds[0][slot][q.off + k];
+        const uint32_t* lC0 = &lds[0][slot][UW + q.off + k];
+        gload();
+        lstore(0);
         wave_lds_fence();
-#ifdef LKX_JPF
-        // J rows are prefetched one row ahead (the DPP broadcast needs the data at once)
-        jrow += jstride;
-        u3a4 jnext = load_jrow_part(jrow, k);
-#endif
 #pragma unroll 2
         for (int y = 0; y < kWin; y++) {
             const int buf = y & 1;
-            if (y + 1 < kWin) gload(v0 + y + 1, true);
+            if (y + 1 < kWin) gload();
             uint32_t rj[11];
-#ifdef LKX_JPF
-            const u3a4 jcur = jnext;
-            jrow += jstride;
-            if (y + 1 < kWin) jnext = load_jrow_part(jrow, k);
-            bcast_jrow(jcur, rj);
-#elif defined(LKX_NOBUF)
-            jrow += jstride;
-            load_jrow_quad(jrow, k, rj);
-#else
             joff += (uint32_t)pitch;
             {
                 const v3u m = __builtin_amdgcn_raw_buffer_load_b96(jrs, (int)joff, 0, 0);
@@ -420,26 +541,25 @@ void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
                 mm.x = m.x; mm.y = m.y; mm.z = m.z;
                 bcast_jrow(mm, rj);
             }
-#endif
             const uint32_t* ld = lD0 + buf * LBUF;
             const uint32_t* lc = lC0 + buf * LBUF;
 #pragma unroll
-            for (int g = 0; g < 10; g++) {
-                pb[g] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[g + 1], rj[g], sel));
+            for (int gi = 0; gi < 10; gi++) {
+                pb[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
                 // (J*32 - I*32) exactly as the reference's CV_DESCALE(...) - I
-                const int jd = __builtin_amdgcn_sdot2(pa[g], W0, __builtin_amdgcn_sdot2(pb[g], W1, (int)lc[4 * g], false),
+                const int jd = __builtin_amdgcn_sdot2(pa[gi], W0, __builtin_amdgcn_sdot2(pb[gi], W1, (int)lc[4 * gi], false),
                                                       false) >> 9;
+                const uint32_t d = ld[4 * gi];
                 const float fd = (float)jd;
-                const uint32_t d = ld[4 * g];
                 const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
                 acc = acc + f * fd;
-                pa[g] = pb[g];
+                pa[gi] = pb[gi];
             }
-            if (y + 1 < kWin) lstore(buf ^ 1, true);
+            if (y + 1 < kWin) lstore(buf ^ 1);
             wave_lds_fence();
         }
         if (!act) acc = f2{0.f, 0.f};
-        // b = (P0+P2) + (P1+P3) across the quad; inactive quads compute garbage they ignore
+        // b = (P0+P2) + (P1+P3) across the quad; inactive quads compute values they ignore
         const float b1s = (quad_bcast<0>(acc.x) + quad_bcast<2>(acc.x)) + (quad_bcast<1>(acc.x) + quad_bcast<3>(acc.x));
         const float b2s = (quad_bcast<0>(acc.y) + quad_bcast<2>(acc.y)) + (quad_bcast<1>(acc.y) + quad_bcast<3>(acc.y));
         if (act) {
@@ -455,9 +575,6 @@ void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
             ny = ny + dy;
             npx = nx + HALFW;
             npy = ny + HALFW;
-#ifdef LKX_FIXED   // timing-only builds (scripts/lk_variants.sh): a fixed iteration count
-            if (j + 1 >= LKX_FIXED) act = false;
-#else
             if ((double)dx * dx + (double)dy * dy <= a.eps2) {
                 act = false;
             } else if (j > 0 && fabs((double)fabsf(dx + pdx)) < 0.01 && fabs((double)fabsf(dy + pdy)) < 0.01) {
@@ -465,41 +582,128 @@ void k_lk_level(LkArgs a, const uint8_t* __restrict__ cls, int level)
                 npy = npy - dy * 0.5f;
                 act = false;
             }
-#endif
             pdx = dx;
             pdy = dy;
         }
-    }
-    if (level == 0 && valid && status) {
-        const int fx = (int)floorf(npx - HALFW), fy = (int)floorf(npy - HALFW);
-        if (fx < -kWin || fx >= L.w || fy < -kWin || fy >= L.h) status = 0;
-    }
-    if (a.dbg && valid && k == 0)
-        a.dbg[((long long)pair * a.g.nlev + level) * a.npts + pt] = make_float4(npx, npy, (float)iters, (float)status);
-    if (valid && k == 0) {
-        reinterpret_cast<float2*>(a.next_pts)[po] = make_float2(npx, npy);
-        if (level == 0) a.status[po] = (uint8_t)status;
+        if (live) {
+            j++;
+            if ((__ballot(act) & smask) == 0 || j >= a.max_iters) {
+                live = false;
+                retire();
+            }
+        }
     }
 }
 
-hipError_t launch_lk_v2(hipStream_t s, int batch, const LkArgs& a, uint8_t* cls)
+// persistent waves for k_lk_iter: what the device keeps resident at once
+template <int G, int UW>
+static int lk_iter_resident()
 {
-    for (int l = a.maxl; l >= 0; l--) {
-        // class planes of this level right before its use: they are still in L2 / MALL
-        const ClassLevel& C = a.plan.lv[l];
-        LkClassArgs ca;
-        ca.g = a.g;
-        ca.plan = a.plan;
-        ca.rlist = a.rlist;
-        ca.level = l;
-        const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.UH, batch * C.nrx * C.nry);
-        hipLaunchKernelGGL(k_lk_class, grid, dim3(64), 0, s, a.pyr1, a.der, cls, ca);
-        const dim3 lg(((C.nxp + 15) / 16) * a.ny, batch);
-        switch (a.plan.nch) {
-        case 1: hipLaunchKernelGGL(k_lk_level<1>, lg, dim3(64), 0, s, a, cls, l); break;
-        case 2: hipLaunchKernelGGL(k_lk_level<2>, lg, dim3(64), 0, s, a, cls, l); break;
-        case 4: hipLaunchKernelGGL(k_lk_level<4>, lg, dim3(64), 0, s, a, cls, l); break;
-        default: return hipErrorInvalidValue;
+    static int cached = 0;
+    if (!cached) {
+        int dev = 0, ncu = 0, nb = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lk_iter<G, UW>, 64, 0);
+        cached = std::max(1, ncu) * std::max(1, nb);
+    }
+    return cached;
+}
+
+template <int G, int UW>
+static int lk_groups(const LkArgs& a, int l)
+{
+    return (a.plan.lv[l].nxp / G) * a.ny;
+}
+
+template <int G, int UW>
+static void launch_A(hipStream_t s, int batch, const LkArgs& a, const uint8_t* cls, float4* Ab, int* qctr, int l)
+{
+    constexpr int S = LkShape<G, UW>::S;
+    const int ngroups = lk_groups<G, UW>(a, l);
+    hipLaunchKernelGGL((k_lk_A<G, UW>), dim3((ngroups + S - 1) / S, batch), dim3(64), 0, s, a, cls, Ab, qctr, l,
+                       ngroups);
+}
+
+template <int G, int UW>
+static void launch_iter(hipStream_t s, int batch, const LkArgs& a, const uint8_t* cls, const float4* Ab, int* qctr,
+                        int l)
+{
+    constexpr int S = LkShape<G, UW>::S;
+    const int ngroups = lk_groups<G, UW>(a, l);
+    // persistent waves, a multiple of 8 so that every XCD range has waves
+    const int need = (int)std::min<long long>(((long long)batch * ngroups + S - 1) / S, 1 << 30);
+    const int W = std::max(8, std::min((need + 7) / 8, lk_iter_resident<G, UW>() / 8) * 8);
+    hipLaunchKernelGGL((k_lk_iter<G, UW>), dim3(W), dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups, batch);
+}
+
+hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
+                        float4* Ab, int* qctr)
+{
+    // An XCD range spans at most ceil(n/8) + 1 pairs; its class slabs (and pyramids) must stay
+    // addressable by 32-bit buffer offsets, so very large batches of large frames run in
+    // sub-batches (the plan already guarantees one pair's slab fits).
+    const long long span = std::max(a.plan.bytes_per_pair, a.g.img_bytes);
+    int sub = batch;
+    while (sub > 1 && ((sub + 7) / 8 + 1) * span > 0x7fff0000LL) sub = std::max(1, sub / 2);
+    if (const char* e = std::getenv("MDX_LK_SUB")) sub = std::max(1, std::min(sub, std::atoi(e)));   // tests
+    // Class planes and A sums depend on the previous frame only, not on the flow: with an aux
+    // stream they run ahead (level L-1's while level L iterates, filling that kernel's tail);
+    // every level has its own class planes, A buffer and queue heads, so nothing is overwritten
+    // while still in use.
+    hipStream_t sa = aux ? aux : s;
+    for (int p = 0, si = 0; p < batch; p += sub, si++) {
+        const int nb = std::min(sub, batch - p);
+        LkArgs b = a;
+        b.pyr1 = a.pyr1 + (long long)p * a.g.img_bytes;
+        b.pyr2 = a.pyr2 + (long long)p * a.g.img_bytes;
+        b.der = a.der + (long long)p * a.g.der_words;
+        b.next_pts = a.next_pts + (long long)p * a.npts * 2;
+        b.status = a.status + (long long)p * a.npts;
+        if (p) b.dbg = nullptr;   // the trace covers the first sub-batch
+        uint8_t* bcls = cls + (long long)p * a.plan.bytes_per_pair;
+        int* bq = qctr + si * kMaxLevels * 8;
+        if (aux) {
+            if (hipError_t e = hipEventRecord(ev[kMaxLevels], s)) return e;
+            if (hipError_t e = hipStreamWaitEvent(sa, ev[kMaxLevels], 0)) return e;
+        }
+        for (int l = a.maxl; l >= 0; l--) {
+            const ClassLevel& C = a.plan.lv[l];
+            LkClassArgs ca;
+            ca.g = a.g;
+            ca.plan = a.plan;
+            ca.rlist = a.rlist;
+            ca.level = l;
+            const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.UH, nb * C.nrx * C.nry);
+            hipLaunchKernelGGL(k_lk_class, grid, dim3(64), 0, sa, b.pyr1, b.der, bcls, ca);
+            float4* bA = Ab + ((long long)l * batch + p) * a.npts;
+            const int G = C.G, UW = C.UW;
+            switch (G * 1000 + UW) {
+            case 4064: launch_A<4, 64>(sa, nb, b, bcls, bA, bq, l); break;
+            case 4128: launch_A<4, 128>(sa, nb, b, bcls, bA, bq, l); break;
+            case 8128: launch_A<8, 128>(sa, nb, b, bcls, bA, bq, l); break;
+            case 8256: launch_A<8, 256>(sa, nb, b, bcls, bA, bq, l); break;
+            case 8512: launch_A<8, 512>(sa, nb, b, bcls, bA, bq, l); break;
+            default: return hipErrorInvalidValue;
+            }
+            if (aux) {
+                if (hipError_t e = hipEventRecord(ev[l], sa)) return e;
+            }
+        }
+        for (int l = a.maxl; l >= 0; l--) {
+            const ClassLevel& C = a.plan.lv[l];
+            if (aux) {
+                if (hipError_t e = hipStreamWaitEvent(s, ev[l], 0)) return e;
+            }
+            const float4* bA = Ab + ((long long)l * batch + p) * a.npts;
+            switch (C.G * 1000 + C.UW) {
+            case 4064: launch_iter<4, 64>(s, nb, b, bcls, bA, bq, l); break;
+            case 4128: launch_iter<4, 128>(s, nb, b, bcls, bA, bq, l); break;
+            case 8128: launch_iter<8, 128>(s, nb, b, bcls, bA, bq, l); break;
+            case 8256: launch_iter<8, 256>(s, nb, b, bcls, bA, bq, l); break;
+            case 8512: launch_iter<8, 512>(s, nb, b, bcls, bA, bq, l); break;
+            default: return hipErrorInvalidValue;
+            }
         }
     }
     return hipGetLastError();

@@ -17,5 +17,5 @@ run() {  # name, extra rocprof args...
 run stats --stats
 run sq --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU
 run cache --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum
-run mem --pmc FETCH_SIZE WRITE_SIZE
+[ -n "$PROBE_MEM" ] && run mem --pmc FETCH_SIZE WRITE_SIZE
 exit 0

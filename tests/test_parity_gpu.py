@@ -143,9 +143,19 @@ def test_warp_diff_dev_batch(mdx, ctx, oracle):
         assert int((out[i] != ref).sum()) == 0, f"pair {i}"
 
 
-def test_batch_dev_matches_host_path(mdx, oracle):
+@pytest.mark.parametrize("B,env", [
+    (4, {}),
+    # 11 pairs: the LK queue's 8 per-XCD ranges split pairs; sub-batches of 3; both group sizes
+    (11, {"MDX_LK_SUB": "3"}),
+    (11, {"MDX_LK_G": "4"}),
+    (11, {"MDX_LK_G": "8"}),
+    (5, {"MDX_LK_AUX": "0"}),   # class / A kernels on the main stream
+])
+def test_batch_dev_matches_host_path(mdx, oracle, monkeypatch, B, env):
     """The zero-copy batched entry gives the same per-pair results as the oracle."""
-    w, h, B = 320, 240, 4
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    w, h = 320, 240
     pairs = [mdx.synth_pair(300 + i, w, h, 1) for i in range(B)]
     g1 = np.stack([p[0] for p in pairs]); g2 = np.stack([p[1] for p in pairs])
     n = mdx.grid_count(w, h, 10)
