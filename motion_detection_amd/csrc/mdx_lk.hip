@@ -43,6 +43,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace mdx {
 
@@ -126,6 +127,26 @@ __device__ __forceinline__ void wave_lds_fence()
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #endif
+}
+
+// timing-only builds (scripts/lk_variants.sh): LKX_MEMFREE re-reads one row (cache-resident) in
+// the iteration kernel, which bounds what hiding the load latency could gain
+#ifdef LKX_MEMFREE
+#define LKX_ROWSTEP(x) 0u
+#else
+#define LKX_ROWSTEP(x) (x)
+#endif
+
+#ifndef LKX_DMA
+#define LKX_DMA 1   // LDS-DMA row pipeline in k_lk_iter for single-load unions (0: register staging)
+#endif
+typedef __attribute__((address_space(3))) void* lds_ptr;
+// s_waitcnt vmcnt(0) (gfx9 encoding: expcnt / lgkmcnt left at their maxima), pinned in place
+__device__ __forceinline__ void lk_vmcnt0()
+{
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs; remap so that each
@@ -374,7 +395,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     constexpr float FLT_SCALE = 1.f / (1 << 20);
     constexpr int SW = 2 * UW + Sh::SPAD;                         // words per slot: D row, C row, pad
     constexpr int LBUF = S * SW;                                  // words per LDS buffer
-    __shared__ __attribute__((aligned(16))) uint32_t lds[2][S][SW];
+    // register-staged rows (NL > 1) / LDS-DMA rows (NL == 1): [buf][D, C][slot][UW], [buf][quad][12]
+    __shared__ __attribute__((aligned(16))) uint32_t lds[NL == 1 && LKX_DMA ? 1 : 2][S][NL == 1 && LKX_DMA ? 1 : SW];
+    __shared__ __attribute__((aligned(16))) uint32_t dU[2][2][NL == 1 && LKX_DMA ? S * UW : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t dJ[2][NL == 1 && LKX_DMA ? 256 : 1];
 
     const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
     const unsigned long long smask = ((1ull << LPS) - 1) << (slot * LPS);
@@ -434,7 +458,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
             const v4u u = __builtin_amdgcn_raw_buffer_load_b128(crs, vo, csoff, 0);
             rc[c] = make_uint4(u.x, u.y, u.z, u.w);
         }
-        roff += rowb;
+        roff += LKX_ROWSTEP(rowb);
     };
     auto lstore = [&](int buf) {
 #pragma unroll
@@ -511,52 +535,142 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         const s2 W1 = {(short)v10, (short)v11};
         const int o = (inx & 3) + k;
         const unsigned sel = (unsigned)o | 0x0c00u | ((unsigned)(o + 1) << 16) | 0x0c000000u;
-        uint32_t joff = jrel + jbase + (uint32_t)(iny * pitch + (inx & ~3) + 12 * k);   // this lane's J dwords
+        // this lane's J dwords: 3 (register path, DPP-shared) or 4 (LDS-DMA: a dwordx3 LDS-DMA
+        // still advances 16 B per lane in LDS, so lanes load 16 B and the quad's first 12 dwords
+        // land contiguously)
+        constexpr bool kDma = NL == 1 && LKX_DMA;
+        uint32_t joff = jrel + jbase + (uint32_t)(iny * pitch + (inx & ~3) + (kDma ? 16 : 12) * k);
         // taps of the current window row (pa) are the previous row's lower taps (pb)
         s2 pa[10], pb[10];
-        {
-            const v3u m = __builtin_amdgcn_raw_buffer_load_b96(jrs, (int)joff, 0, 0);
-            u3a4 mm;
-            mm.x = m.x; mm.y = m.y; mm.z = m.z;
-            uint32_t rj[11];
-            bcast_jrow(mm, rj);
-#pragma unroll
-            for (int gi = 0; gi < 10; gi++) pa[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
-        }
-        roff = q.dlane + (uint32_t)q.v0 * rowb;
-        const uint32_t* lD0 = &lds[0][slot][q.off + k];
-        const uint32_t* lC0 = &lds[0][slot][UW + q.off + k];
-        gload();
-        lstore(0);
-        wave_lds_fence();
-#pragma unroll 2
-        for (int y = 0; y < kWin; y++) {
-            const int buf = y & 1;
-            if (y + 1 < kWin) gload();
-            uint32_t rj[11];
-            joff += (uint32_t)pitch;
-            {
-                const v3u m = __builtin_amdgcn_raw_buffer_load_b96(jrs, (int)joff, 0, 0);
-                u3a4 mm;
-                mm.x = m.x; mm.y = m.y; mm.z = m.z;
-                bcast_jrow(mm, rj);
-            }
-            const uint32_t* ld = lD0 + buf * LBUF;
-            const uint32_t* lc = lC0 + buf * LBUF;
+        auto row_math = [&](const uint32_t (&rj)[11], const uint32_t (&dv)[10], const uint32_t (&cv)[10]) {
 #pragma unroll
             for (int gi = 0; gi < 10; gi++) {
                 pb[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
                 // (J*32 - I*32) exactly as the reference's CV_DESCALE(...) - I
-                const int jd = __builtin_amdgcn_sdot2(pa[gi], W0, __builtin_amdgcn_sdot2(pb[gi], W1, (int)lc[4 * gi], false),
+                const int jd = __builtin_amdgcn_sdot2(pa[gi], W0, __builtin_amdgcn_sdot2(pb[gi], W1, (int)cv[gi], false),
                                                       false) >> 9;
-                const uint32_t d = ld[4 * gi];
                 const float fd = (float)jd;
-                const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
+                const f2 f = {(float)(int16_t)dv[gi], (float)((int)dv[gi] >> 16)};
                 acc = acc + f * fd;
                 pa[gi] = pb[gi];
             }
-            if (y + 1 < kWin) lstore(buf ^ 1);
+        };
+        if constexpr (NL == 1 && LKX_DMA) {
+            // Rows arrive by LDS-DMA (buffer_load ... lds): per row the slot's union segments of D
+            // and C (one dwordx4 per lane; the wave's lanes fill [slot][UW] in order) and each lane
+            // quad's J row segment (dwordx4 per lane, 12 of the quad's 16 dwords used).  A row's loads are issued one row ahead and
+            // retired by an explicit vmcnt(0) at the top of the next row (the compiler does not
+            // track LDS-DMA); no staging registers, no ds_write, no DPP broadcast of J.
+            uint32_t uoff = q.dlane + (uint32_t)q.v0 * rowb;
+            auto dma_union = [&](int b) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)&dU[b][0][0], 16, (int)uoff, 0, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)&dU[b][1][0], 16, (int)uoff, csoff, 0, 0);
+                uoff += LKX_ROWSTEP(rowb);
+            };
+            auto dma_j = [&](int b) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(jrs, (lds_ptr)&dJ[b][0], 16, (int)joff, 0, 0, 0);
+                joff += LKX_ROWSTEP((uint32_t)pitch);
+            };
+            const uint32_t* lJ = &dJ[0][(lane >> 2) * 16];
+            auto read_j = [&](int b, uint32_t (&rj)[11]) {
+                const uint4 j0 = *reinterpret_cast<const uint4*>(lJ + b * 256);
+                const uint4 j1 = *reinterpret_cast<const uint4*>(lJ + b * 256 + 4);
+                const uint4 j2 = *reinterpret_cast<const uint4*>(lJ + b * 256 + 8);
+                rj[0] = j0.x; rj[1] = j0.y; rj[2] = j0.z; rj[3] = j0.w;
+                rj[4] = j1.x; rj[5] = j1.y; rj[6] = j1.z; rj[7] = j1.w;
+                rj[8] = j2.x; rj[9] = j2.y; rj[10] = j2.z;
+            };
+            const uint32_t* lD = &dU[0][0][slot * UW + q.off + k];
+            constexpr int UB = 2 * S * UW;                            // words per union buffer
+            dma_union(0);
+            dma_j(0);
+            dma_j(1);
+            lk_vmcnt0();
+            {
+                uint32_t rj[11];
+                read_j(0, rj);
+#pragma unroll
+                for (int gi = 0; gi < 10; gi++) pa[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
+            }
+            // two rows per step with constant buffers; the taps alternate between pa and pb
+            // (no copies), and an opaque use of acc pins each row's arithmetic before the next
+            // row's wait
+            auto row = [&](int y, auto bc, s2 (&up)[10], s2 (&lo)[10]) {
+                constexpr int b = decltype(bc)::value;
+                if (y) lk_vmcnt0();                                   // union row y, J row y+1
+                uint32_t rj[11], dv[10], cv[10];
+                read_j(b ^ 1, rj);
+#pragma unroll
+                for (int gi = 0; gi < 10; gi++) {
+                    dv[gi] = lD[b * UB + 4 * gi];
+                    cv[gi] = lD[b * UB + S * UW + 4 * gi];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (y + 1 < kWin) dma_union(b ^ 1);
+                if (y + 2 <= kWin) dma_j(b);                          // J row y+2 over row y (read at y-1)
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int gi = 0; gi < 10; gi++) {
+                    lo[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
+                    // (J*32 - I*32) exactly as the reference's CV_DESCALE(...) - I
+                    const int jd = __builtin_amdgcn_sdot2(up[gi], W0, __builtin_amdgcn_sdot2(lo[gi], W1, (int)cv[gi], false),
+                                                          false) >> 9;
+                    const float fd = (float)jd;
+                    const f2 f = {(float)(int16_t)dv[gi], (float)((int)dv[gi] >> 16)};
+                    acc = acc + f * fd;
+                }
+                asm volatile("" : "+v"(acc));
+            };
+#pragma unroll 1
+            for (int y = 0; y < kWin; y += 2) {
+                row(y, std::integral_constant<int, 0>{}, pa, pb);
+                row(y + 1, std::integral_constant<int, 1>{}, pb, pa);
+            }
+        } else {
+            {
+                const v3u m = __builtin_amdgcn_raw_buffer_load_b96(jrs, (int)joff, 0, 0);
+                u3a4 mm;
+                mm.x = m.x; mm.y = m.y; mm.z = m.z;
+                uint32_t rj[11];
+                bcast_jrow(mm, rj);
+#pragma unroll
+                for (int gi = 0; gi < 10; gi++) pa[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
+            }
+            roff = q.dlane + (uint32_t)q.v0 * rowb;
+            const uint32_t* lD0 = &lds[0][slot][q.off + k];
+            const uint32_t* lC0 = &lds[0][slot][UW + q.off + k];
+            gload();
+            lstore(0);
             wave_lds_fence();
+#pragma unroll 2
+            for (int y = 0; y < kWin; y++) {
+                const int buf = y & 1;
+                // J row first: its use right below then waits for it alone (vmcnt retires in
+                // order), while the next union row stays in flight through this row's arithmetic
+                uint32_t rj[11];
+                joff += LKX_ROWSTEP((uint32_t)pitch);
+                const v3u jm = __builtin_amdgcn_raw_buffer_load_b96(jrs, (int)joff, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (y + 1 < kWin) gload();
+                __builtin_amdgcn_sched_barrier(0);
+                {
+                    u3a4 mm;
+                    mm.x = jm.x; mm.y = jm.y; mm.z = jm.z;
+                    bcast_jrow(mm, rj);
+                }
+                const uint32_t* ld = lD0 + buf * LBUF;
+                const uint32_t* lc = lC0 + buf * LBUF;
+                uint32_t dv[10], cv[10];
+#pragma unroll
+                for (int gi = 0; gi < 10; gi++) {
+                    dv[gi] = ld[4 * gi];
+                    cv[gi] = lc[4 * gi];
+                }
+                row_math(rj, dv, cv);
+                __builtin_amdgcn_sched_barrier(0);   // keep the staging store (and its wait) after the arithmetic
+                if (y + 1 < kWin) lstore(buf ^ 1);
+                wave_lds_fence();
+            }
         }
         if (!act) acc = f2{0.f, 0.f};
         // b = (P0+P2) + (P1+P3) across the quad; inactive quads compute values they ignore
@@ -575,6 +689,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
             ny = ny + dy;
             npx = nx + HALFW;
             npy = ny + HALFW;
+#ifdef LKX_FIXED   // timing-only builds: every trackable point iterates exactly LKX_FIXED times
+            if (j + 1 >= LKX_FIXED) act = false;
+#else
             if ((double)dx * dx + (double)dy * dy <= a.eps2) {
                 act = false;
             } else if (j > 0 && fabs((double)fabsf(dx + pdx)) < 0.01 && fabs((double)fabsf(dy + pdy)) < 0.01) {
@@ -582,6 +699,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
                 npy = npy - dy * 0.5f;
                 act = false;
             }
+#endif
             pdx = dx;
             pdy = dy;
         }
