@@ -74,6 +74,16 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def allgather_bytes(self, b: bytes) -> list:
+        """Every rank's equal-length byte string, in rank order (the row-tiled path's record
+        exchange: 96 B per rank, host-side over gloo)."""
+        if self.dist is None:
+            return [b]
+        t = self.torch.frombuffer(bytearray(b), dtype=self.torch.uint8)
+        out = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [bytes(o.numpy().tobytes()) for o in out]
+
     def close(self):
         if self.dist is not None:
             self.dist.destroy_process_group()

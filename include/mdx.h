@@ -131,6 +131,43 @@ int mdx_warp_diff_dev(mdx_ctx* ctx, int batch, const uint8_t* d_gray1, const uin
                       int w, int h, int stride, size_t frame_stride,
                       const double* d_H, uint8_t* d_mask);
 
+/*
+ * Row-tiled path: one frame pair split by rows over several GPUs (8K RGB
+ * over 8 GPUs).  No reference interface corresponds -- the reference runs the whole frame in one
+ * calculateOpticalFlow call (optical_flow_calculator.cpp:30-130); this splits that call at its
+ * only global step, the first-four-accepted getPerspectiveTransform input (:118-120).
+ *
+ * Rank r owns the destination rows [y0, y1) (the bands partition [0, h)) and the grid points
+ * whose row y = gy*pixel_step lies in that band.  Per pair:
+ *   1. every rank: mdx_band_flow_dev -- rows A1-A6 for the band's points.  next_pts / status /
+ *      vectors are full-frame arrays ([npts]...); only the band's entries are written.  d_cand
+ *      receives the band's mdx_band_cand record.
+ *   2. the caller all-gathers the ranks' records (any transport: RCCL all_gather over xGMI, or
+ *      host memory) into one device array, in any order.
+ *   3. every rank: mdx_band_fit_warp_dev -- the first four accepted points overall are the four
+ *      smallest indices over all records; the fit, its inverse and num_vectors are then exactly
+ *      the full path's.  Writes mask rows [y0, y1) to d_mask_band (row pitch w) and, when
+ *      non-NULL, d_H[9] and d_num_vectors.
+ * Both entries are asynchronous on the context stream and reuse the context's pyramids, so
+ * step 3 must follow step 1 on the same context with no other call in between.  fit_mode must
+ * be MDX_FIT_FIRST4.
+ */
+typedef struct mdx_band_cand {
+    int32_t count;     /* accepted vectors (status && |d| > min_vector_size) in the band */
+    int32_t n;         /* min(count, 4) */
+    int32_t idx[4];    /* x-major grid index k = gx*ny + gy of the band's first n accepted points */
+    float src[8];      /* their grid positions (x, y) */
+    float dst[8];      /* their tracked positions next_pts[k] */
+    int32_t pad_[2];
+} mdx_band_cand;       /* 96 bytes */
+
+int mdx_band_flow_dev(mdx_ctx* ctx, const uint8_t* d_img1, const uint8_t* d_img2,
+                      int w, int h, int stride, int fmt, int y0, int y1,
+                      float* d_next_pts, uint8_t* d_status, double* d_vectors,
+                      mdx_band_cand* d_cand);
+int mdx_band_fit_warp_dev(mdx_ctx* ctx, int nrec, const mdx_band_cand* d_cands, int y0, int y1,
+                          uint8_t* d_mask_band, double* d_H, int* d_num_vectors);
+
 /* Device memory helpers so hosts without a HIP toolchain (ctypes, cgo, JNI) can stage
  * buffers: allocation on the context's device, copies ordered on its stream. */
 void* mdx_dev_alloc(mdx_ctx* ctx, size_t bytes);

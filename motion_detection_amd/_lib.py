@@ -33,8 +33,18 @@ EXPORTED = [
     "mdx_device_sync",
     "mdx_flow_warp_diff", "mdx_flow_warp_diff_batch_dev", "mdx_warp_diff_dev", "mdx_dev_alloc",
     "mdx_dev_free", "mdx_memcpy_h2d", "mdx_memcpy_d2h", "mdx_enable_timing", "mdx_timing_calls", "mdx_stage_ms",
-    "mdx_synth_pair", "mdx_debug_copy",
+    "mdx_synth_pair", "mdx_debug_copy", "mdx_band_flow_dev", "mdx_band_fit_warp_dev",
 ]
+
+
+class MdxBandCand(C.Structure):
+    """mdx_band_cand (include/mdx.h): one row band's accepted count and first four accepted points."""
+    _fields_ = [("count", C.c_int32), ("n", C.c_int32), ("idx", C.c_int32 * 4), ("src", C.c_float * 8),
+                ("dst", C.c_float * 8), ("pad_", C.c_int32 * 2)]
+
+
+BAND_CAND_BYTES = 96
+assert C.sizeof(MdxBandCand) == BAND_CAND_BYTES
 
 
 class MdxParams(C.Structure):
@@ -116,6 +126,10 @@ def lib() -> C.CDLL:
     L.mdx_debug_copy.restype = C.c_int
     L.mdx_synth_pair.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, u8p, u8p, f64p, C.c_int]
     L.mdx_synth_pair.restype = C.c_int
+    L.mdx_band_flow_dev.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp]
+    L.mdx_band_flow_dev.restype = C.c_int
+    L.mdx_band_fit_warp_dev.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, vp, vp, vp]
+    L.mdx_band_fit_warp_dev.restype = C.c_int
     _lib = L
     return L
 

@@ -126,6 +126,19 @@ class Context:
         return self._check(lib().mdx_warp_diff_dev(self._h, batch, C.c_void_p(d_gray1), C.c_void_p(d_gray2), w, h,
                                                    stride, frame_stride, C.c_void_p(d_H), C.c_void_p(d_mask)))
 
+    # -- row-tiled path (one pair split by rows over ranks; include/mdx.h mdx_band_*)
+    def band_flow_dev(self, d_img1: int, d_img2: int, w: int, h: int, stride: int, fmt: int, y0: int, y1: int,
+                      d_next_pts: int, d_status: int, d_cand: int, d_vectors: int = 0) -> int:
+        v = lambda x: C.c_void_p(x) if x else None  # noqa: E731
+        return self._check(lib().mdx_band_flow_dev(self._h, v(d_img1), v(d_img2), w, h, stride, fmt, y0, y1,
+                                                   v(d_next_pts), v(d_status), v(d_vectors), v(d_cand)))
+
+    def band_fit_warp_dev(self, nrec: int, d_cands: int, y0: int, y1: int, d_mask_band: int, d_H: int = 0,
+                          d_num_vectors: int = 0) -> int:
+        v = lambda x: C.c_void_p(x) if x else None  # noqa: E731
+        return self._check(lib().mdx_band_fit_warp_dev(self._h, nrec, v(d_cands), y0, y1, v(d_mask_band), v(d_H),
+                                                       v(d_num_vectors)))
+
     def sync(self):
         self._check(lib().mdx_sync(self._h))
 

@@ -40,7 +40,8 @@ struct mdx_ctx {
     bool lk_debug = false;
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
-    int plan_w = -1, plan_h = -1, plan_ps = -1, plan_ml = -1;
+    int plan_w = -1, plan_h = -1, plan_ps = -1, plan_ml = -1, plan_gy0 = -1, plan_gy1 = -1;
+    int band_w = 0, band_h = 0;              // frame of the last mdx_band_flow_dev (its pyramids are live)
     ClassPlan plan{};
     bool timing = false;
     static constexpr int kSlots = 256;     // timed calls kept between mdx_enable_timing and readout
@@ -130,7 +131,7 @@ static int ensure(mdx_ctx* c, DevBuf& b, size_t need)
     if (need == 0) need = 1;
     if (b.p && b.cap >= need) return MDX_OK;
     if (b.p) {
-        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->stream);   // the aux stream's work is always joined by c->stream
         (void)hipFree(b.p);
         b.p = nullptr;
         b.cap = 0;
@@ -157,10 +158,11 @@ static int ensure_workspace(mdx_ctx* c, const Geometry& g, int batch)
 // the class-plane layout.  Rebuilt and uploaded only when frame size / pixel_step / levels change.
 // plan.nch == 0 means some group's union is wider than 512 columns (pixel_step >~ 66) or a pair's
 // class slab exceeds 2 GB: the caller then runs the single-kernel LK instead.
-static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps, int batch)
+static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps, int batch, int gy0, int gy1)
 {
     int rc;
-    if (c->plan_w != w || c->plan_h != h || c->plan_ps != ps || c->plan_ml != g.nlev) {
+    if (c->plan_w != w || c->plan_h != h || c->plan_ps != ps || c->plan_ml != g.nlev || c->plan_gy0 != gy0 ||
+        c->plan_gy1 != gy1) {
         const int nx = (w + ps - 1) / ps, ny = (h + ps - 1) / ps;
         static_assert(kMaxLevels <= 8, "residue tables sized for 2^7 residues");
         std::vector<int16_t> tab(2 * kMaxLevels * 2 * 128, (int16_t)-1);
@@ -220,18 +222,29 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
                 for (size_t q = r.size(); q % C.G; q++) ord.push_back((int16_t)-1);
             }
             C.nxp = (int)ord.size() - C.ord_off;
-            // rows: grouped by class the same way (no padding: a group is one row)
+            // rows of the band [gy0, gy1): grouped by class the same way (no padding: a group is
+            // one row)
             const size_t r0 = ord.size();
-            for (int i = 0; i < ny; i++) ord.push_back((int16_t)i);
+            for (int i = gy0; i < gy1; i++) ord.push_back((int16_t)i);
             const int16_t* cmy = cmap + (l * 2 + 1) * 128;
             std::stable_sort(ord.begin() + r0, ord.end(),
                              [&](int16_t u, int16_t v) { return cmy[(u * ps) & m] < cmy[(v * ps) & m]; });
         }
+        (void)ny;
         long long off = 0;
         for (int l = 0; l < g.nlev; l++) {
             ClassLevel& C = P.lv[l];
             C.UH = g.lv[l].h + 79;
             C.PW = (g.lv[l].w + kPad + std::max(C.UW, 64) + 3) & ~3;
+            // plane rows the band's windows read: first rows v0 = clamp(ipy + 40, 0, UH - 40) of
+            // its first and last grid rows (ipy is monotone in gy), 40 rows each
+            const float scale = (float)(1. / (1 << l));
+            auto v0_of = [&](int gy) {
+                const int ipy = (int)std::floor((float)(gy * ps) * scale - 19.5f);
+                return std::min(std::max(ipy + kPad, 0), C.UH - kWin);
+            };
+            C.vlo = v0_of(gy0);
+            C.vhi = v0_of(gy1 - 1) + kWin;
             C.class_bytes = (long long)C.UH * C.PW * 8;
             C.off = off;
             off += (long long)C.nrx * C.nry * C.class_bytes;
@@ -242,12 +255,17 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
         P.bytes_per_pair = (off + 255) / 256 * 256;
         tab.insert(tab.end(), ord.begin(), ord.end());
         if ((rc = ensure(c, c->ctab, tab.size() * sizeof(int16_t))) != MDX_OK) return rc;
+        // kernels of earlier calls may still read the old tables: the copy waits for them (the
+        // stream is non-blocking, so a plain hipMemcpy would not)
+        HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
         HIP_OR_RETURN(c, hipMemcpy(c->ctab.p, tab.data(), tab.size() * sizeof(int16_t), hipMemcpyHostToDevice));
         c->plan = P;
         c->plan_w = w;
         c->plan_h = h;
         c->plan_ps = ps;
         c->plan_ml = g.nlev;
+        c->plan_gy0 = gy0;
+        c->plan_gy1 = gy1;
     }
     if (c->plan.nch == 0) return MDX_OK;
     if ((rc = ensure(c, c->cls, (size_t)c->plan.bytes_per_pair * batch + 64)) != MDX_OK) return rc;
@@ -406,9 +424,12 @@ static inline void mark(mdx_ctx* c, int i)
 }
 
 // The pipeline on device buffers.  d_np/d_st must be valid (LK writes them).
+// Row-band mode (cand != null, batch 1): LK and classification for grid rows [gy0, gy1) only, the
+// band's record to *cand, no fit and no mask.
 static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint8_t* d_img2, int w, int h, int stride,
                         size_t frame_stride, int fmt, float* d_np, uint8_t* d_st, double* d_vec, uint8_t* d_mask,
-                        double* d_H, const double* d_Hext, int* d_num)
+                        double* d_H, const double* d_Hext, int* d_num, int gy0 = 0, int gy1 = -1,
+                        mdx_band_cand* cand = nullptr)
 {
     const mdx_params& P = c->prm;
     if (w <= 0 || h <= 0 || batch <= 0) return set_err(c, MDX_EINVAL, "bad frame size or batch");
@@ -423,6 +444,8 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
     if (rc != MDX_OK) return rc;
     const int npts = mdx_grid_count(w, h, P.pixel_step);
     const int ny = (h + P.pixel_step - 1) / P.pixel_step;
+    if (gy1 < 0) gy1 = ny;
+    const int nyb = gy1 - gy0;
     hipStream_t s = c->stream;
     uint8_t* pyr1 = c->pyr1.as<uint8_t>();
     uint8_t* pyr2 = c->pyr2.as<uint8_t>();
@@ -436,7 +459,7 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
     mark(c, 2);
     for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, batch, pyr1, der, g, l));
     mark(c, 3);
-    if (npts > 0) {
+    if (npts > 0 && nyb > 0) {
         LkArgs a{};
         a.pyr1 = pyr1;
         a.pyr2 = pyr2;
@@ -445,6 +468,7 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         a.maxl = g.nlev - 1;
         a.npts = npts;
         a.ny = ny;
+        a.nyg = nyb;
         a.pixel_step = P.pixel_step;
         a.max_iters = std::min(std::max(P.max_iters, 0), 100);
         a.min_eig = P.min_eig;
@@ -454,10 +478,12 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         a.status = d_st;
         bool v2 = c->lk_impl == 2;
         if (v2) {
-            if ((rc = ensure_class_plan(c, g, w, h, P.pixel_step, batch)) != MDX_OK) return rc;
+            if ((rc = ensure_class_plan(c, g, w, h, P.pixel_step, batch, gy0, gy1)) != MDX_OK) return rc;
             v2 = c->plan.nch != 0;   // very sparse grids: the single-kernel LK
         }
         if (!v2) {
+            if (gy0 != 0 || gy1 != ny)
+                return set_err(c, MDX_EINVAL, "row bands need the class-plane LK (pixel_step too large)");
             HIP_OR_RETURN(c, launch_lk(s, batch, a));
         } else {
             a.plan = c->plan;
@@ -479,9 +505,13 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
     }
     mark(c, 4);
     if ((rc = ensure(c, c->csum, classify_scratch_bytes(batch, npts))) != MDX_OK) return rc;
-    HIP_OR_RETURN(c, launch_classify_fit(s, batch, d_np, d_st, npts, ny, P.pixel_step, P.min_vector_size, d_vec, fits,
-                                         P.fit_mode, d_Hext, c->csum.p));
+    HIP_OR_RETURN(c, launch_classify_fit(s, batch, d_np, d_st, npts, ny, gy0, gy1, P.pixel_step, P.min_vector_size, d_vec,
+                                         fits, P.fit_mode, d_Hext, c->csum.p, cand));
     mark(c, 5);
+    if (cand) {
+        mark(c, 6);
+        return MDX_OK;
+    }
     if (d_mask) {
         const Level& L0 = g.lv[0];
         const uint8_t* g1 = pyr1 + L0.img_off + L0.core();
@@ -583,6 +613,50 @@ extern "C" int mdx_warp_diff_dev(mdx_ctx* c, int batch, const uint8_t* d_gray1, 
                                       (long long)frame_stride, stride, w, h, fits, d_mask, (long long)w * h,
                                       c->prm.thresh));
     mark(c, 6);
+    return MDX_OK;
+}
+
+extern "C" int mdx_band_flow_dev(mdx_ctx* c, const uint8_t* d_img1, const uint8_t* d_img2, int w, int h, int stride,
+                                 int fmt, int y0, int y1, float* d_next_pts, uint8_t* d_status, double* d_vectors,
+                                 mdx_band_cand* d_cand)
+{
+    if (!c) return MDX_EINVAL;
+    if (!d_img1 || !d_img2 || !d_next_pts || !d_status || !d_cand)
+        return set_err(c, MDX_EINVAL, "mdx_band_flow_dev: null pointer");
+    if (w <= 0 || h <= 0 || y0 < 0 || y1 > h || y0 >= y1) return set_err(c, MDX_EINVAL, "bad band [%d, %d) of %d rows", y0, y1, h);
+    if (c->prm.fit_mode != MDX_FIT_FIRST4) return set_err(c, MDX_EINVAL, "row bands need fit_mode FIRST4");
+    const int ps = c->prm.pixel_step;
+    // grid rows whose y = gy*ps lies in [y0, y1)
+    const int gy0 = (y0 + ps - 1) / ps, gy1 = (y1 + ps - 1) / ps;
+    c->band_w = c->band_h = 0;
+    const int rc = run_pipeline(c, 1, d_img1, d_img2, w, h, stride, (size_t)stride * h, fmt, d_next_pts, d_status,
+                                d_vectors, nullptr, nullptr, nullptr, nullptr, gy0, gy1, d_cand);
+    if (rc == MDX_OK) {
+        c->band_w = w;
+        c->band_h = h;
+    }
+    return rc;
+}
+
+extern "C" int mdx_band_fit_warp_dev(mdx_ctx* c, int nrec, const mdx_band_cand* d_cands, int y0, int y1,
+                                     uint8_t* d_mask_band, double* d_H, int* d_num_vectors)
+{
+    if (!c) return MDX_EINVAL;
+    if (nrec <= 0 || !d_cands || !d_mask_band) return set_err(c, MDX_EINVAL, "mdx_band_fit_warp_dev: bad argument");
+    const int w = c->band_w, h = c->band_h;
+    if (w <= 0 || h <= 0) return set_err(c, MDX_EINVAL, "mdx_band_fit_warp_dev: no mdx_band_flow_dev before");
+    if (y0 < 0 || y1 > h || y0 >= y1) return set_err(c, MDX_EINVAL, "bad band [%d, %d) of %d rows", y0, y1, h);
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    const Geometry g = make_geometry(w, h, c->prm.max_level);
+    hipStream_t s = c->stream;
+    PairFit* fits = c->fits.as<PairFit>();
+    HIP_OR_RETURN(c, launch_band_fit(s, nrec, d_cands, fits));
+    const Level& L0 = g.lv[0];
+    const uint8_t* g1 = c->pyr1.as<uint8_t>() + L0.img_off + L0.core();
+    const uint8_t* g2 = c->pyr2.as<uint8_t>() + L0.img_off + L0.core();
+    HIP_OR_RETURN(c, launch_warp_diff(s, 1, g1, g.img_bytes, L0.pitch, g2, g.img_bytes, L0.pitch, w, h, fits, d_mask_band,
+                                      (long long)w * (y1 - y0), c->prm.thresh, y0, y1));
+    if (d_H || d_num_vectors) HIP_OR_RETURN(c, launch_export_fit(s, 1, fits, d_H, d_num_vectors));
     return MDX_OK;
 }
 

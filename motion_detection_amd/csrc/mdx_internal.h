@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mdx.h"
+
 namespace mdx {
 
 constexpr int kMaxLevels = 8;
@@ -52,6 +54,7 @@ struct ClassLevel {
     int ord_off;             // offset of this level's order tables in LkArgs::ord
     int G;                   // points per LK group (4 or 8)
     int UW;                  // union columns per group (64, 128, 256 or 512)
+    int vlo, vhi;            // plane rows the planned grid rows' windows reach (k_lk_class range)
 };
 
 struct ClassPlan {
@@ -74,6 +77,7 @@ struct LkArgs {
     Geometry g;
     int maxl;                // attained max level used by LK
     int npts, ny, pixel_step;
+    int nyg;                 // LK v2: grid rows in the group order (ny, or a row band's count)
     int max_iters;
     float min_eig;
     double eps2;
@@ -100,15 +104,23 @@ hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
 // + 1 events (no timing) used to order the two streams.
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
                         float4* Ab, int* qctr);
+// Grid rows [gy0, gy1) only (a row band; others are neither written nor counted).  cand != null:
+// row-band mode -- the band's count and first four accepted points go to *cand (one record per
+// pair) instead of a fit.
 hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
-                               int ny, int pixel_step, double min_vector_size, double* vectors, PairFit* fits,
-                               int fit_mode, const double* H_external, void* scratch);
+                               int ny, int gy0, int gy1, int pixel_step, double min_vector_size, double* vectors,
+                               PairFit* fits, int fit_mode, const double* H_external, void* scratch,
+                               mdx_band_cand* cand);
+// Merge nrec band records (first four accepted overall = four smallest indices) and fit
+hipError_t launch_band_fit(hipStream_t s, int nrec, const mdx_band_cand* cands, PairFit* fit);
 // bytes of the scratch launch_classify_fit needs
 inline size_t classify_scratch_bytes(int batch, int npts) { return (size_t)batch * ((npts + 255) / 256) * 32; }
 hipError_t launch_set_fit_external(hipStream_t s, int batch, const double* H_external, PairFit* fits);
+// Destination rows [row0, row1) of every pair (row1 <= h); mask row y is at mask + (y - row0) * w.
 hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,
                             const uint8_t* g2, long long g2_stride, int g2_pitch, int w, int h,
-                            const PairFit* fits, uint8_t* mask, long long mask_stride, int thresh);
+                            const PairFit* fits, uint8_t* mask, long long mask_stride, int thresh, int row0 = 0,
+                            int row1 = -1);
 hipError_t launch_export_fit(hipStream_t s, int batch, const PairFit* fits, double* H, int* num_vectors);
 
 }  // namespace mdx

@@ -648,14 +648,15 @@ struct BlockSummary {
 };
 
 __global__ __launch_bounds__(256) void k_classify(const float* __restrict__ next_pts, const uint8_t* __restrict__ status,
-                                                  int npts, int ny, int pixel_step, double mvs,
+                                                  int npts, int ny, int gy0, int gy1, int pixel_step, double mvs,
                                                   double* __restrict__ vectors, BlockSummary* __restrict__ summ)
 {
     const int pair = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     __shared__ int s_wcnt[4];
     const int i = blk * 256 + tid;
     bool acc = false;
-    if (i < npts) {
+    const int gyi = i % ny;
+    if (i < npts && gyi >= gy0 && gyi < gy1) {   // grid rows of the band (all rows: the full path)
         const float sx = (float)((i / ny) * pixel_step), sy = (float)((i % ny) * pixel_step);
         const float2 e = reinterpret_cast<const float2*>(next_pts)[(long long)pair * npts + i];
         double v0, v1, v2, v3;
@@ -745,6 +746,96 @@ __global__ __launch_bounds__(64) void k_fit(const float* __restrict__ next_pts, 
     }
 }
 
+// Row-band mode: the same block scan as k_fit, but the band's count and first four accepted
+// points go to its record (the fit waits for every band's record, k_band_fit).
+__global__ __launch_bounds__(64) void k_band_record(const float* __restrict__ next_pts, int npts, int ny, int pixel_step,
+                                                    const BlockSummary* __restrict__ summ, int nblk,
+                                                    mdx_band_cand* __restrict__ cand)
+{
+    const int pair = blockIdx.x, lane = threadIdx.x;
+    const BlockSummary* S = summ + (long long)pair * nblk;
+    int carry = 0;
+    int pick[4] = {-1, -1, -1, -1};
+    for (int b0 = 0; b0 < nblk; b0 += 64) {
+        const int b = b0 + lane;
+        const int cnt = b < nblk ? S[b].count : 0;
+        int incl = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int t = __shfl_up(incl, d);
+            if (lane >= d) incl += t;
+        }
+        const int excl = carry + incl - cnt;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const bool here = cnt > 0 && r >= excl && r < excl + cnt;
+            const unsigned long long m = __ballot(here);
+            if (m) {
+                const int src = __ffsll((long long)m) - 1;
+                const int v = here ? S[b].first[r - excl] : 0;
+                const int got = __shfl(v, src);
+                if (pick[r] < 0) pick[r] = got;
+            }
+        }
+        carry += __shfl(incl, 63);
+    }
+    if (lane != 0) return;
+    mdx_band_cand& c = cand[pair];
+    c.count = carry;
+    c.n = carry < 4 ? carry : 4;
+    for (int r = 0; r < 4; r++) {
+        const int i = r < c.n ? pick[r] : -1;
+        c.idx[r] = i;
+        if (i >= 0) {
+            c.src[2 * r] = (float)((i / ny) * pixel_step);
+            c.src[2 * r + 1] = (float)((i % ny) * pixel_step);
+            const float2 e = reinterpret_cast<const float2*>(next_pts)[(long long)pair * npts + i];
+            c.dst[2 * r] = e.x;
+            c.dst[2 * r + 1] = e.y;
+        } else {
+            c.src[2 * r] = c.src[2 * r + 1] = c.dst[2 * r] = c.dst[2 * r + 1] = 0.f;
+        }
+    }
+    c.pad_[0] = c.pad_[1] = 0;
+}
+
+// Merge the bands' records: the four smallest indices over all records are the frame's first four
+// accepted points (each band lists its own first four, and bands partition the points), so the
+// fit below is bit-identical to the full path's k_fit.
+__global__ void k_band_fit(const mdx_band_cand* __restrict__ cands, int nrec, PairFit* __restrict__ fit)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int total = 0;
+    int best[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};
+    float bs[8] = {}, bd[8] = {};
+    for (int r = 0; r < nrec; r++) {
+        const mdx_band_cand& c = cands[r];
+        total += c.count;
+        for (int q = 0; q < c.n && q < 4; q++) {
+            int i = c.idx[q];
+            float sx = c.src[2 * q], sy = c.src[2 * q + 1], dx = c.dst[2 * q], dy = c.dst[2 * q + 1];
+            for (int k = 0; k < 4; k++) {   // insertion into the sorted four
+                if (i < best[k]) {
+                    const int ti = best[k];
+                    const float t0 = bs[2 * k], t1 = bs[2 * k + 1], t2 = bd[2 * k], t3 = bd[2 * k + 1];
+                    best[k] = i; bs[2 * k] = sx; bs[2 * k + 1] = sy; bd[2 * k] = dx; bd[2 * k + 1] = dy;
+                    i = ti; sx = t0; sy = t1; dx = t2; dy = t3;
+                }
+            }
+        }
+    }
+    PairFit& f = *fit;
+    f.num_vectors = total;
+    if (total >= 4) {
+        dev_perspective_fit(bs, bd, f.H);
+        dev_invert3x3(f.H, f.Hinv);
+        f.fit_status = 0;
+    } else {
+        for (int k = 0; k < 9; k++) { f.H[k] = 0.0; f.Hinv[k] = 0.0; }
+        f.fit_status = total == 0 ? 1 : 2;
+    }
+}
+
 __global__ void k_set_fit_external(const double* __restrict__ H_ext, PairFit* __restrict__ fits, int batch)
 {
     const int pair = blockIdx.x * blockDim.x + threadIdx.x;
@@ -807,15 +898,25 @@ hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a)
 }
 
 hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
-                               int ny, int pixel_step, double mvs, double* vectors, PairFit* fits, int fit_mode,
-                               const double* H_external, void* scratch)
+                               int ny, int gy0, int gy1, int pixel_step, double mvs, double* vectors, PairFit* fits,
+                               int fit_mode, const double* H_external, void* scratch, mdx_band_cand* cand)
 {
     const int nblk = (npts + 255) / 256;
     BlockSummary* summ = reinterpret_cast<BlockSummary*>(scratch);
-    hipLaunchKernelGGL(k_classify, dim3(nblk, batch), dim3(256), 0, s, next_pts, status, npts, ny, pixel_step, mvs,
-                       vectors, summ);
-    hipLaunchKernelGGL(k_fit, dim3(batch), dim3(64), 0, s, next_pts, npts, ny, pixel_step, summ, nblk, fits, fit_mode,
-                       H_external);
+    if (nblk > 0)
+        hipLaunchKernelGGL(k_classify, dim3(nblk, batch), dim3(256), 0, s, next_pts, status, npts, ny, gy0, gy1,
+                           pixel_step, mvs, vectors, summ);
+    if (cand)
+        hipLaunchKernelGGL(k_band_record, dim3(batch), dim3(64), 0, s, next_pts, npts, ny, pixel_step, summ, nblk, cand);
+    else
+        hipLaunchKernelGGL(k_fit, dim3(batch), dim3(64), 0, s, next_pts, npts, ny, pixel_step, summ, nblk, fits,
+                           fit_mode, H_external);
+    return hipGetLastError();
+}
+
+hipError_t launch_band_fit(hipStream_t s, int nrec, const mdx_band_cand* cands, PairFit* fit)
+{
+    hipLaunchKernelGGL(k_band_fit, dim3(1), dim3(64), 0, s, cands, nrec, fit);
     return hipGetLastError();
 }
 

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
     const int nclass = C.nrx * C.nry;
     const int pair = blockIdx.z / nclass, cls = blockIdx.z % nclass;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    const int v = blockIdx.y;
+    const int v = C.vlo + blockIdx.y;                // only rows some planned window reaches
     // columns a window can reach: x = u - 40 <= w + 38; the rest of PW is union-load slack whose
     // values no lane uses, so it is left unwritten
     if (4 * j >= a.g.lv[level].w + 2 * kPad || v >= C.UH) return;
@@ -270,7 +270,7 @@ __device__ __forceinline__ GroupGeom group_geom(const LkArgs& a, const ClassLeve
     const int16_t* yo = xo + C.nxp;
     const bool has = g >= 0;
     const int gg = has ? g : 0;
-    const int cg = gg / a.ny, row = gg - cg * a.ny;   // column-group major: neighbours share rows
+    const int cg = gg / a.nyg, row = gg - cg * a.nyg;   // column-group major: neighbours share rows
     const int e0 = cg * G;
     const int gxv = has ? xo[e0 + (sl >> 2)] : -1;
     r.valid = gxv >= 0;
@@ -731,7 +731,7 @@ static int lk_iter_resident()
 template <int G, int UW>
 static int lk_groups(const LkArgs& a, int l)
 {
-    return (a.plan.lv[l].nxp / G) * a.ny;
+    return (a.plan.lv[l].nxp / G) * a.nyg;
 }
 
 template <int G, int UW>
@@ -792,7 +792,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             ca.plan = a.plan;
             ca.rlist = a.rlist;
             ca.level = l;
-            const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.UH, nb * C.nrx * C.nry);
+            const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.vhi - C.vlo, nb * C.nrx * C.nry);
             hipLaunchKernelGGL(k_lk_class, grid, dim3(64), 0, sa, b.pyr1, b.der, bcls, ca);
             float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             const int G = C.G, UW = C.UW;

@@ -104,9 +104,9 @@ struct TileInfo {
 
 // Bounds of the tile's taps, computed on lanes 0..3 (one corner each) with the reference
 // arithmetic; fast = every |X|, |Y| < 2^30 (no clamp, magic rounding exact) and the footprint fits.
-__device__ TileInfo tile_info(const double* M, double Wd, int x0, int y0, int w, int h, int lane)
+__device__ TileInfo tile_info(const double* M, double Wd, int x0, int y0, int w, int yend, int lane)
 {
-    const int cxl = min(kWTile - 1, w - 1 - x0), cyl = min(kHTile - 1, h - 1 - y0);
+    const int cxl = min(kWTile - 1, w - 1 - x0), cyl = min(kHTile - 1, yend - 1 - y0);
     const int c = lane & 3;
     const int x1 = (c & 1) ? cxl : 0, y = y0 + ((c & 2) ? cyl : 0);
     const double X0 = M[0] * x0 + M[1] * y + M[2];
@@ -153,7 +153,7 @@ __device__ __forceinline__ void warp_rows(lds_d2* s_xy, lds_u8* s_src, int r0, i
                                           const double* ty, double Wd, double mX, double mY, uint32_t bias)
 {
     const uint8_t* g2r = g2p + (long long)(y0 + r0) * g2_pitch + xs;
-    uint8_t* mr = mp + (long long)(y0 + r0) * w + xs;
+    uint8_t* mr = mp + (long long)(y0 + r0) * w + xs;   // mp: mask row 0 of the pair's band, shifted by -row0
     const long long g2s = 4LL * g2_pitch, ms = 4LL * w;
     for (int i = 0; i < nrows; i++, g2r += g2s, mr += ms) {
         const d2v xy = s_xy[r0 + 4 * i];
@@ -233,13 +233,15 @@ __device__ __forceinline__ void warp_rows(lds_d2* s_xy, lds_u8* s_src, int r0, i
     }
 }
 
-// grid: x -> tile column, y -> tile row, z -> pair.  256 threads; lane l of wave q owns columns
-// x0 + 4*(l & 15) .. +3 of tile rows 32q + (l >> 4) + 4i, i = 0..7.
+// grid: x -> tile column, y -> tile row of the band [row0, row1), z -> pair.  256 threads; lane l
+// of wave q owns columns x0 + 4*(l & 15) .. +3 of tile rows 32q + (l >> 4) + 4i, i = 0..7.  The
+// reference's blocking depends on the full height only through bw0, and each pixel's arithmetic
+// on (x, y) only, so a band is exactly the full frame's rows.
 __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
                                                    const uint8_t* __restrict__ g2, long long g2_stride, int g2_pitch,
                                                    int w, int h, int bw0, const PairFit* __restrict__ fits,
                                                    uint8_t* __restrict__ mask, long long mask_stride, int thresh,
-                                                   int vec_ok)
+                                                   int vec_ok, int row0, int row1)
 {
     __shared__ __attribute__((aligned(16))) double s_xy[kHTile][2];    // (X0, Y0) per tile row
     __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
@@ -257,13 +259,13 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     }
     const int pair = bid / (nbx * nby), tile = bid - pair * (nbx * nby);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int x0 = (tile % nbx) * kWTile, y0 = (tile / nbx) * kHTile;
+    const int x0 = (tile % nbx) * kWTile, y0 = row0 + (tile / nbx) * kHTile;
     const int cq = lane & 15, rr = lane >> 4;
     const int xs = x0 + 4 * cq;                     // this lane's 4 columns
     const int r0 = (kHTile / 4) * wave + rr;        // this lane's first tile row
-    const int nrows = max(0, min(kHTile / 16, (h - y0 - r0 + 3) >> 2));
+    const int nrows = max(0, min(kHTile / 16, (row1 - y0 - r0 + 3) >> 2));
     const uint8_t* g2p = g2 + (long long)pair * g2_stride;
-    uint8_t* mp = mask + (long long)pair * mask_stride;
+    uint8_t* mp = mask + (long long)pair * mask_stride - (long long)row0 * w;   // indexed by frame row
 
     const PairFit& f = fits[pair];
     if (f.fit_status != 0) {   // no fit: the reference produces no mask; ours is all zero
@@ -284,7 +286,7 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     const bool try_fast = affine && bw0 == kWTile && vec_ok && x0 + kWTile <= w;
 
     if (try_fast && wave == 0) {
-        const TileInfo t = tile_info(M, Wd, x0, y0, w, h, lane);
+        const TileInfo t = tile_info(M, Wd, x0, y0, w, row1, lane);
         if (lane == 0) s_info = t;
     }
     if (try_fast) __syncthreads();
@@ -364,16 +366,18 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
 
 hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,
                             const uint8_t* g2, long long g2_stride, int g2_pitch, int w, int h, const PairFit* fits,
-                            uint8_t* mask, long long mask_stride, int thresh)
+                            uint8_t* mask, long long mask_stride, int thresh, int row0, int row1)
 {
+    if (row1 < 0) row1 = h;
+    if (row0 < 0 || row1 > h || row0 >= row1) return hipErrorInvalidValue;
     const int bh0 = h < 16 ? h : 16;
     const int bw0 = (1024 / bh0) < w ? (1024 / bh0) : w;
     // dword loads of gray2 / stores of the mask need 4-B aligned rows
     const int vec_ok = ((uintptr_t)g2 % 4 == 0) && g2_stride % 4 == 0 && g2_pitch % 4 == 0 &&
                        ((uintptr_t)mask % 4 == 0) && mask_stride % 4 == 0 && w % 4 == 0;
-    const dim3 grid((w + kWTile - 1) / kWTile, (h + kHTile - 1) / kHTile, batch);
+    const dim3 grid((w + kWTile - 1) / kWTile, (row1 - row0 + kHTile - 1) / kHTile, batch);
     hipLaunchKernelGGL(k_warp_diff, grid, dim3(256), 0, s, g1, g1_stride, g1_pitch, g2, g2_stride, g2_pitch, w, h, bw0,
-                       fits, mask, mask_stride, thresh, vec_ok);
+                       fits, mask, mask_stride, thresh, vec_ok, row0, row1);
     return hipGetLastError();
 }
 
