@@ -33,7 +33,7 @@ import motion_detection_amd as mdx  # noqa: E402  (loads libmdx.so before torch,
 
 METRIC = "Mpixels/s (flow+warp+diff) at 1080p & 4K; % HBM roofline, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
-CONFIGS = {"640": (640, 480), "1080p": (1920, 1080), "4k": (3840, 2160)}
+CONFIGS = {"640": (640, 480), "1080p": (1920, 1080), "4k": (3840, 2160), "8k": (7680, 4320)}
 SEED0 = 20141105
 
 
@@ -127,6 +127,126 @@ def cpu_baseline(uniq, w, h, seconds: float, threads: int):
                        f"{el:.1f} s wall")
 
 
+def open_ctx(D: Dist, w: int, h: int, batch: int, **params):
+    """One context on this rank's GPU.  Ranks beyond the visible devices share them round-robin
+    (rehearsing a multi-rank run on a one-GPU box)."""
+    try:
+        return mdx.Context(D.local_rank, w, h, batch, **params)
+    except mdx.MdxError as e:
+        if "out of range" not in str(e):
+            raise
+        log(f"rank {D.rank}: device {D.local_rank} not visible, sharing device 0")
+        return mdx.Context(0, w, h, batch, **params)
+
+
+def main_c4(args, D: Dist, threads: int):
+    """Config C4: one 8K RGB pair row-tiled over the ranks.  `--bands K` splits the frame
+    into K bands dealt round-robin to the ranks (K > ranks rehearses a K-GPU split on fewer GPUs).
+    Per step: each rank runs its bands' flow, the 96-byte band records are all-gathered (gloo,
+    host side), then each rank fits (identically) and writes its bands' mask rows.  Strong scaling:
+    the frame is fixed, `value` = frame pixels / max-over-ranks step time."""
+    from motion_detection_amd import rowtile
+    w, h = CONFIGS[args.config] if args.config != "1080p" else CONFIGS["8k"]
+    ps, fmt = 10, mdx.FMT_RGB8
+    K = args.bands or D.world
+    mine = list(range(D.rank, K, D.world))
+    per_rank = -(-K // D.world)
+    a, b, _ = mdx.synth_pair(SEED0 + 4, w, h, 3, threads)       # every rank: the same frame pair
+    ctx = open_ctx(D, w, h, 1, pixel_step=ps, min_vector_size=1.0)
+    n = mdx.grid_count(w, h, ps)
+    d = {k: ctx.dev_alloc(sz) for k, sz in dict(i1=a.nbytes, i2=b.nbytes, np=n * 8, st=n, cand=per_rank * 96,
+                                               cands=K * 96, mask=w * h, num=4).items()}
+    ctx.h2d(d["i1"], a)
+    ctx.h2d(d["i2"], b)
+    rows = [rowtile.band_rows(h, K, k) for k in range(K)]
+    pad = bytes(96)
+    t_ph = {"flow": 0.0, "exchange": 0.0, "fit_warp": 0.0}
+
+    def step(timed=False):
+        t0 = time.perf_counter()
+        for j, k in enumerate(mine):
+            ctx.band_flow_dev(d["i1"], d["i2"], w, h, w * 3, fmt, *rows[k], d["np"], d["st"], d["cand"] + 96 * j)
+        rec = np.empty(per_rank * 96, np.uint8)
+        ctx.d2h(rec, d["cand"])                                  # synchronous: the flow is done
+        t1 = time.perf_counter()
+        local = rec.tobytes()[:96 * len(mine)] + pad * (per_rank - len(mine))
+        parts = D.allgather_bytes(local)
+        allrec = bytearray(K * 96)
+        for r, part in enumerate(parts):                         # rank r holds bands r, r + world, ...
+            for j, k in enumerate(range(r, K, D.world)):
+                allrec[96 * k:96 * (k + 1)] = part[96 * j:96 * (j + 1)]
+        ctx.h2d(d["cands"], np.frombuffer(bytes(allrec), np.uint8))
+        t2 = time.perf_counter()
+        for k in mine:
+            ctx.band_fit_warp_dev(K, d["cands"], *rows[k], d["mask"] + rows[k][0] * w, 0, d["num"])
+        ctx.sync()
+        t3 = time.perf_counter()
+        if timed:
+            t_ph["flow"] += t1 - t0
+            t_ph["exchange"] += t2 - t1
+            t_ph["fit_warp"] += t3 - t2
+
+    for _ in range(args.warmup):
+        step()
+    D.barrier()
+    ctx.device_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed=True)
+    ctx.device_sync()
+    D.barrier()
+    el = time.perf_counter() - t0
+    el_max = D.max(el)
+    num = np.empty(1, np.int32)
+    ctx.d2h(num, d["num"])
+    # one band alone (K bands on K GPUs: each GPU's share), timed here for the rehearsal case
+    band_ms, band_stages = None, None
+    if K > D.world and mine:
+        k = mine[0]
+        reps = max(2, args.steps)
+        ctx.device_sync()
+        ctx.enable_timing(True)
+        tb = time.perf_counter()
+        for _ in range(reps):
+            ctx.band_flow_dev(d["i1"], d["i2"], w, h, w * 3, fmt, *rows[k], d["np"], d["st"], d["cand"])
+            ctx.band_fit_warp_dev(K, d["cands"], *rows[k], d["mask"] + rows[k][0] * w, 0, d["num"])
+        ctx.device_sync()
+        band_ms = (time.perf_counter() - tb) / reps * 1e3
+        st = ctx.stage_ms()
+        band_stages = {kk: round(v / max(st["calls"], 1), 4) for kk, v in st.items() if kk != "calls"}
+    for p in d.values():
+        ctx.dev_free(p)
+    out = {
+        "metric": METRIC,
+        "value": round(args.steps * w * h / el_max / 1e6, 2),
+        "unit": "Mpixels/s",
+        "n_gpus": D.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el_max / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (mdx_synth_pair, rgb8)",
+        "config": {"workload": f"C4: one {w}x{h} RGB pair per step, row-tiled into {K} bands over "
+                               f"{D.world} rank(s); per band LK + classify, one 96-B record all-gather, "
+                               f"identical fit on every rank, band warp+absdiff+threshold",
+                   "frame": f"{w}x{h}", "pixel_step": ps, "bands": K, "bands_per_rank": per_rank,
+                   "parallelism": f"row bands, {D.world} rank(s), record exchange over gloo (host)"},
+        "phase_ms_per_step_rank0": {k: round(v / args.steps * 1e3, 3) for k, v in t_ph.items()},
+        "one_band_ms": round(band_ms, 3) if band_ms else None,
+        "one_band_stage_ms": band_stages,
+        "num_vectors": int(num[0]),
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+    if D.rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    D.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -143,14 +263,19 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_warp_diff.json"),
                     help="per-launch HBM traffic measured by rocprofv3 --pmc (scripts/profile.sh)")
+    ap.add_argument("--workload", default="c1", choices=["c1", "c4"],
+                    help="c1: batched 1080p stream shards (the metric's config); c4: 8K RGB row-tiled")
+    ap.add_argument("--bands", type=int, default=0, help="c4: row bands (default: one per rank)")
     args = ap.parse_args()
 
     D = Dist()
     if args.gpus != D.world:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {D.world}; using WORLD_SIZE")
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    if args.workload == "c4":
+        return main_c4(args, D, threads)
     w, h = CONFIGS[args.config]
-    B = args.batch or {"640": 128, "1080p": 32, "4k": 8}[args.config]
+    B = args.batch or {"640": 128, "1080p": 32, "4k": 8, "8k": 2}[args.config]
     unique = max(1, min(args.unique, B))
     ps = 10
 
