@@ -43,8 +43,9 @@ struct PairFit {
 };
 
 // Residue-class planes of LK v2 (mdx_lk.hip): per level, one plane set per class of
-// (P_x mod 2^L, P_y mod 2^L) present in the grid.  Each class holds two row-major UH x PW arrays:
-// D (uint32, Ix | Iy << 16) then C (int32, 256 - 512*I: the J-chain bias, see mdx_lk.hip).
+// (P_x mod 2^L, P_y mod 2^L) present in the grid.  Each class holds one row-major UH x PW array of
+// 8-B (D, C) pairs: D (uint32, Ix | Iy << 16) and C (int32, 256 - 512*I: the J-chain bias, see
+// mdx_lk.hip).
 struct ClassLevel {
     int nrx, nry;            // residue classes per axis
     int UH, PW;              // plane rows (h + 79), plane width in elements (multiple of 4)

@@ -10,8 +10,8 @@
 //              grid point's window origin prevPt - 19.5 has a fractional part fixed by
 //              (P mod 2^L), so all points of a residue class share the bilinear weights: the
 //              16x-overlapping per-window interpolation of the reference becomes one
-//              interpolation per class and pixel.  Natural row-major layout, two arrays per
-//              class: D = (Ix | Iy << 16) and C = 256 - 512*I (the J-chain bias, see below).
+//              interpolation per class and pixel.  Row-major (D, C) pairs per class and plane
+//              column: D = (Ix | Iy << 16) and C = 256 - 512*I (the J-chain bias, see below).
 //  k_lk_A      Per point: the gradient matrix sums A11/A12/A22 over the window and the minEig /
 //              determinant tests.
 //  k_lk_iter   The Newton iterations, on persistent waves fed from per-XCD work queues.
@@ -30,7 +30,7 @@
 // row, and every lane then reads its 10 chain elements from LDS.  That replaces the 6 scattered
 // dwordx2/x4 loads per lane and row that bound a per-point design on the texture data path (TD
 // busy 97%, VALU 38%).  J (the moving window in the next frame) differs per point: its row
-// segment is loaded once per lane quad (3 dwords per lane) and shared by DPP.
+// segment is loaded once per lane quad and read back from LDS by the quad's lanes.
 //
 // Arithmetic: J taps via v_perm_b32 + v_dot2_i32_i16 (signed weights: w11 may be -1);
 // dot2(pa, W0, dot2(pb, W1, C)) >> 9 == ((S + 256) >> 9) - I exactly, because C = 256 - 512*I
@@ -49,9 +49,7 @@ namespace mdx {
 
 typedef short s2 __attribute__((ext_vector_type(2)));
 typedef float f2 __attribute__((ext_vector_type(2)));
-// 4-B aligned multi-dword loads (global_load_dwordx4/x3 at dword-aligned addresses)
-struct __attribute__((aligned(4))) u4a4 { uint32_t x, y, z, w; };
-struct __attribute__((aligned(4))) u3a4 { uint32_t x, y, z; };
+// 4-B aligned 8-byte loads (global_load_dwordx2 at dword-aligned addresses)
 struct __attribute__((aligned(4))) u2a4 { uint32_t x, y; };
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
@@ -95,26 +93,6 @@ __device__ __forceinline__ uint32_t quad_bcast_u(uint32_t v)
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xf, 0xf, false);
 }
 
-// One J row segment of a point's window, shared by its lane quad: the 11 dwords from the
-// 4-B aligned column B = inx & ~3 cover every lane's taps (lane k needs bytes o + 4g and
-// o + 4g + 1 with o = (inx & 3) + k <= 6, i.e. inside dwords g, g+1).  Each lane loads 3 of
-// them and DPP broadcasts assemble the row in every lane: 12 B of L1 traffic per lane, not 48.
-__device__ __forceinline__ u3a4 load_jrow_part(const uint32_t* seg, int k)
-{
-    return *reinterpret_cast<const u3a4*>(seg + 3 * k);
-}
-__device__ __forceinline__ void bcast_jrow(const u3a4 m, uint32_t (&r)[11])
-{
-    r[0] = quad_bcast_u<0>(m.x); r[1] = quad_bcast_u<0>(m.y); r[2] = quad_bcast_u<0>(m.z);
-    r[3] = quad_bcast_u<1>(m.x); r[4] = quad_bcast_u<1>(m.y); r[5] = quad_bcast_u<1>(m.z);
-    r[6] = quad_bcast_u<2>(m.x); r[7] = quad_bcast_u<2>(m.y); r[8] = quad_bcast_u<2>(m.z);
-    r[9] = quad_bcast_u<3>(m.x); r[10] = quad_bcast_u<3>(m.y);
-}
-__device__ __forceinline__ void load_jrow_quad(const uint32_t* seg, int k, uint32_t (&r)[11])
-{
-    bcast_jrow(load_jrow_part(seg, k), r);
-}
-
 // Ordering point between a window row's LDS staging writes and the next row's reads.  A
 // workgroup is one wave and one wave's LDS instructions execute in order, so only the compiler
 // must be kept from moving LDS accesses across it (no s_barrier, no forced vmcnt(0)).
@@ -137,15 +115,22 @@ __device__ __forceinline__ void wave_lds_fence()
 #define LKX_ROWSTEP(x) (x)
 #endif
 
-#ifndef LKX_DMA
-#define LKX_DMA 1   // LDS-DMA row pipeline in k_lk_iter for single-load unions (0: register staging)
+#ifndef LKX_WPE_ITER
+#define LKX_WPE_ITER 6   // k_lk_iter: 6 waves/SIMD (<= 80 VGPRs; 6 KiB LDS each fits 24 per CU)
 #endif
 typedef __attribute__((address_space(3))) void* lds_ptr;
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+// volatile LDS views: each access stays one ds_read_b64 / ds_read_b128 (never merged into a
+// half-rate read2 or narrowed)
+typedef __attribute__((address_space(3))) volatile const v2u lds_u2v;
+typedef __attribute__((address_space(3))) volatile const v4u lds_u4v;
 // s_waitcnt vmcnt(0) (gfx9 encoding: expcnt / lgkmcnt left at their maxima), pinned in place
 __device__ __forceinline__ void lk_vmcnt0()
 {
     __builtin_amdgcn_sched_barrier(0);
+#ifndef LKX_NOWAIT   // timing-only builds: measure what the row waits cost (results invalid)
     __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
     __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -222,17 +207,17 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
 #pragma unroll
         for (int q = 0; q < 4; q++) cv[q] = 256;
     }
-    const long long o = (long long)v * C.PW + 4 * j;
-    *reinterpret_cast<uint4*>(reinterpret_cast<uint32_t*>(base) + o) = make_uint4(dv[0], dv[1], dv[2], dv[3]);
-    *reinterpret_cast<int4*>(reinterpret_cast<int32_t*>(base) + (long long)C.UH * C.PW + o) =
-        make_int4(cv[0], cv[1], cv[2], cv[3]);
+    // (D, C) pairs, row-major: one 8-B element per plane column
+    uint4* o = reinterpret_cast<uint4*>(base) + ((long long)v * C.PW + 4 * j) / 2;
+    o[0] = make_uint4(dv[0], (uint32_t)cv[0], dv[1], (uint32_t)cv[1]);
+    o[1] = make_uint4(dv[2], (uint32_t)cv[2], dv[3], (uint32_t)cv[3]);
 }
 
 // ------------------------------------------------------------------ one pyramid level
 // Work units.  A GROUP is G consecutive members of one residue class along one grid row (host
 // order: each class's run padded to a multiple of G with -1).  A SLOT is the 4G lanes holding one
 // group, a lane quad per point.  Per window row a slot needs one contiguous "union" segment of UW
-// plane columns of D (and C): NL coalesced dwordx4 per lane, staged in a double-buffered LDS row.
+// plane columns, UW (D, C) pairs: staged in LDS, from where each lane reads its 10 chain pairs.
 //
 // Per level two kernels follow k_lk_class:
 //  k_lk_A     static groups (one slot each): the gradient sums A11/A12/A22 and the minEig /
@@ -241,15 +226,16 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
 //  k_lk_iter  the Newton iterations.  Points iterate 1..max_iters times; a slot whose G points
 //             iterate in lockstep costs the max over the group, and a static wave the max over
 //             all its groups.  So the waves are persistent and each slot, when its group retires,
-//             takes the next group from a per-(level, pair) atomic counter: slots of one wave
-//             run out of step, only the group-internal lockstep remains.
+//             takes the next group from a work queue: slots of one wave run out of step, only the
+//             group-internal lockstep remains.
 template <int G, int UW>
 struct LkShape {
-    static constexpr int LPS = 4 * G;            // lanes per slot
-    static constexpr int S = 64 / LPS;           // slots per wave
-    static constexpr int NL = UW / (4 * LPS);    // dwordx4 per lane and union row
-    static constexpr int SPAD = 0;               // LDS words per slot row beyond the union
-    static_assert(NL >= 1 && NL * 4 * LPS == UW, "union width must be a multiple of a slot's row load");
+    static constexpr int LPS = 4 * G;               // lanes per slot
+    static constexpr int S = 64 / LPS;              // slots per wave
+    static constexpr int NP = UW / (2 * LPS);       // A pass: 16-B (2-pair) loads per lane and union row
+    static constexpr int ND = S * UW * 8 / 1024;    // iterations: 1-KiB LDS-DMA pieces per union row
+    static_assert(NP >= 1 && NP * 2 * LPS == UW, "union width must be a multiple of a slot's row load");
+    static_assert(ND >= 1 && ND * 1024 == S * UW * 8, "a wave's union row must be whole LDS-DMA pieces");
 };
 
 struct GroupGeom {
@@ -258,7 +244,7 @@ struct GroupGeom {
     int ipx, ipy;     // floor of the window origin at this level
     int off;          // the point's first column inside the union
     int v0;           // first window row in the class plane
-    uint32_t dlane;   // byte offset in the pair's class slab of this lane's union chunk, row 0
+    uint32_t ubase;   // byte offset in the pair's class slab of the union's first pair, plane row 0
 };
 
 // geometry of group g (-1 = none) for lane sl of its slot
@@ -289,20 +275,20 @@ __device__ __forceinline__ GroupGeom group_geom(const LkArgs& a, const ClassLeve
     const int ub = min(max(ipx0 + kPad, 0), C.PW - UW);            // union start column
     r.off = min(max(r.ipx + kPad - ub, 0), UW - kWin);
     r.v0 = min(max(r.ipy + kPad, 0), C.UH - kWin);
-    r.dlane = (uint32_t)(C.off + (long long)(cy * C.nrx + cx) * C.class_bytes) + 4u * (uint32_t)(ub + 4 * sl);
+    r.ubase = (uint32_t)(C.off + (long long)(cy * C.nrx + cx) * C.class_bytes) + 8u * (uint32_t)ub;
     return r;
 }
 
-// ---- A pass.  grid: x -> wave (S static groups), y -> pair (XCD-remapped as one range)
+// ---- A pass.  grid: x -> wave (S static groups), y -> pair (XCD-remapped as one range).  Each
+// lane loads 2 (D, C) pairs per 16-B load and stages the two D words; the chain reads are D only.
 template <int G, int UW>
 __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict__ cls, float4* __restrict__ Ab,
                                              int* __restrict__ qctr, int level, int ngroups)
 {
     using Sh = LkShape<G, UW>;
-    constexpr int LPS = Sh::LPS, S = Sh::S, NL = Sh::NL;
+    constexpr int LPS = Sh::LPS, S = Sh::S, NP = Sh::NP;
     constexpr float FLT_SCALE = 1.f / (1 << 20);
-    constexpr int SW = UW + Sh::SPAD;                             // words per slot row
-    __shared__ __attribute__((aligned(16))) uint32_t lds[2][S][SW];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[2][S][UW];
 
     const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
     const int nw = gridDim.x;
@@ -316,30 +302,31 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
     bool ok = q.valid && !(q.ipx < -kWin || q.ipx >= L.w || q.ipy < -kWin || q.ipy >= L.h);
 
     const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cls + (long long)pair * a.plan.bytes_per_pair, a.plan.bytes_per_pair);
-    const uint32_t rowb = (uint32_t)C.PW * 4;
-    uint32_t roff = q.dlane + (uint32_t)q.v0 * rowb;
+    const uint32_t rowb = (uint32_t)C.PW * 8;
+    uint32_t roff = q.ubase + (uint32_t)q.v0 * rowb + 16u * sl;
     const uint32_t* lD0 = &lds[0][slot][q.off + k];
     // rows are loaded PF ahead (this kernel has few waves' worth of VALU work to hide latency)
     constexpr int PF = 4;
-    uint4 rq[PF][NL];
-    auto gload = [&](uint4 (&rd)[NL]) {
+    uint4 rq[PF][NP];
+    auto gload = [&](uint4 (&rd)[NP]) {
 #pragma unroll
-        for (int c = 0; c < NL; c++) {
+        for (int c = 0; c < NP; c++) {
             const v4u t = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)(roff + 16u * LPS * c), 0, 0);
             rd[c] = make_uint4(t.x, t.y, t.z, t.w);
         }
         roff += rowb;
     };
-    auto lstore = [&](int buf, const uint4 (&rd)[NL]) {
+    auto lstore = [&](int buf, const uint4 (&rd)[NP]) {   // the D word of each (D, C) pair
 #pragma unroll
-        for (int c = 0; c < NL; c++) *reinterpret_cast<uint4*>(&lds[buf][slot][4 * LPS * c + 4 * sl]) = rd[c];
+        for (int c = 0; c < NP; c++)
+            *reinterpret_cast<uint2*>(&lds[buf][slot][2 * (LPS * c + sl)]) = make_uint2(rd[c].x, rd[c].z);
     };
 
     // lane k owns SSE lane k (columns 4g+k), rows in order; ((P0+P1)+P2)+P3 across the quad
     f2 sd = {0.f, 0.f};
     float s12 = 0.f;
     {
-        uint4 r0[NL];
+        uint4 r0[NP];
         gload(r0);
 #pragma unroll
         for (int i = 0; i < PF; i++) gload(rq[i]);
@@ -349,7 +336,7 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
 #pragma unroll
     for (int y = 0; y < kWin; y++) {
         const int buf = y & 1;
-        const uint32_t* ld = lD0 + buf * (S * SW);
+        const uint32_t* ld = lD0 + buf * (S * UW);
 #pragma unroll
         for (int gi = 0; gi < 10; gi++) {
             const uint32_t d = ld[4 * gi];
@@ -384,21 +371,29 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
 // queues spread every XCD over several pairs at once and doubled the L2 misses.  Levels run as
 // separate launches from maxLevel down to 0; the position carried between them is next_pts (the
 // reference's nextPts[ptidx], stored every level).
+//
+// Rows arrive by LDS-DMA (buffer_load ... lds), one row ahead, retired by an explicit vmcnt(0)
+// at the top of the next row (the compiler does not track LDS-DMA):
+//  * the union rows of all S slots: ND pieces of 1 KiB.  A piece's LDS destination is fixed
+//    (lane L writes bytes 16L..16L+15), so lane L of piece c loads the 16 B of whichever slot and
+//    pair offset that position holds in the [slot][UW][D, C] image -- source offsets are
+//    per-lane and refreshed once per iteration;
+//  * each lane quad's J row segment (16 B per lane, 12 of the quad's 16 dwords used).
+// A lane then reads its 10 chain pairs with ds_read_b64 (kept apart: a merged ds_read2_b64
+// would halve the LDS rate) and the quad's J dwords with three ds_read_b128.  D and C travel as
+// one pair, so a chain element is one 2-cycle LDS access (it was two read2_b32 halves).
 template <int G, int UW>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_lk_iter(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER, 8))) void k_lk_iter(
     LkArgs a, const uint8_t* __restrict__ cls, const float4* __restrict__ Ab, int* __restrict__ qctr, int level,
     int ngroups, int batch)
 {
     using Sh = LkShape<G, UW>;
-    constexpr int LPS = Sh::LPS, S = Sh::S, NL = Sh::NL;
+    constexpr int LPS = Sh::LPS, S = Sh::S, ND = Sh::ND;
     constexpr float HALFW = 19.5f;
     constexpr float FLT_SCALE = 1.f / (1 << 20);
-    constexpr int SW = 2 * UW + Sh::SPAD;                         // words per slot: D row, C row, pad
-    constexpr int LBUF = S * SW;                                  // words per LDS buffer
-    // register-staged rows (NL > 1) / LDS-DMA rows (NL == 1): [buf][D, C][slot][UW], [buf][quad][12]
-    __shared__ __attribute__((aligned(16))) uint32_t lds[NL == 1 && LKX_DMA ? 1 : 2][S][NL == 1 && LKX_DMA ? 1 : SW];
-    __shared__ __attribute__((aligned(16))) uint32_t dU[2][2][NL == 1 && LKX_DMA ? S * UW : 1];
-    __shared__ __attribute__((aligned(16))) uint32_t dJ[2][NL == 1 && LKX_DMA ? 256 : 1];
+    constexpr int UB = S * UW;                                    // (D, C) pairs per union buffer
+    __shared__ __attribute__((aligned(16))) uint32_t dU[2][2 * UB];   // [buf][slot][UW][D, C]
+    __shared__ __attribute__((aligned(16))) uint32_t dJ[2][256];      // [buf][quad][16]
 
     const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
     const unsigned long long smask = ((1ull << LPS) - 1) << (slot * LPS);
@@ -411,11 +406,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const ClassLevel& C = a.plan.lv[level];
     const Level L = a.g.lv[level];
     // buffer addressing: descriptors over the range's class slabs and next-frame pyramids (the
-    // host keeps them below 2 GB), 32-bit lane offsets; the C array sits a constant UH*PW*4 bytes
-    // after D (scalar offset field)
+    // host keeps them below 2 GB), 32-bit lane offsets
     const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cls + (long long)p0 * a.plan.bytes_per_pair, np * a.plan.bytes_per_pair);
-    const int csoff = C.UH * C.PW * 4;
-    const uint32_t rowb = (uint32_t)C.PW * 4;
+    const uint32_t rowb = (uint32_t)C.PW * 8;
     const int pitch = L.pitch;
     const __amdgpu_buffer_rsrc_t jrs = buf_rsrc(a.pyr2 + (long long)p0 * a.g.img_bytes, np * a.g.img_bytes);
     const uint32_t jbase = (uint32_t)(L.img_off + L.core());
@@ -447,27 +440,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         }
     };
 
-    uint4 rd[NL], rc[NL];
-    uint32_t roff = 0;
-    auto gload = [&]() {
-#pragma unroll
-        for (int c = 0; c < NL; c++) {
-            const int vo = (int)(roff + 16u * LPS * c);
-            const v4u t = __builtin_amdgcn_raw_buffer_load_b128(crs, vo, 0, 0);
-            rd[c] = make_uint4(t.x, t.y, t.z, t.w);
-            const v4u u = __builtin_amdgcn_raw_buffer_load_b128(crs, vo, csoff, 0);
-            rc[c] = make_uint4(u.x, u.y, u.z, u.w);
-        }
-        roff += LKX_ROWSTEP(rowb);
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int c = 0; c < NL; c++) {
-            *reinterpret_cast<uint4*>(&lds[buf][slot][4 * LPS * c + 4 * sl]) = rd[c];
-            *reinterpret_cast<uint4*>(&lds[buf][slot][UW + 4 * LPS * c + 4 * sl]) = rc[c];
-        }
-    };
-
     for (;;) {
         // ---- refill: each slot without a live group takes the next one; a group with no point
         // left to iterate retires at once
@@ -484,7 +456,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
                     const long long gl = cb + gi;
                     pair = (int)(gl / ngroups);
                     q = group_geom<G, UW>(a, C, level, (int)(gl - (long long)pair * ngroups), sl);
-                    q.dlane += (uint32_t)((long long)(pair - p0) * a.plan.bytes_per_pair);
+                    q.ubase += (uint32_t)((long long)(pair - p0) * a.plan.bytes_per_pair);
                     jrel = (uint32_t)((long long)(pair - p0) * a.g.img_bytes);
                     pt = q.gx * a.ny + q.gy;
                     po = (long long)pair * a.npts + pt;
@@ -518,7 +490,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
 
         // ---- one Newton iteration of every live group.  Lanes that are not iterating (or fail
         // the bounds test) run the row loop on a safe address and drop the result, so the loop
-        // is wave-uniform (it also carries every slot's LDS staging).
+        // is wave-uniform (it also carries every slot's staging).
         f2 acc = {0.f, 0.f};
         if (act) iters++;
         int inx = (int)floorf(nx), iny = (int)floorf(ny);
@@ -535,142 +507,79 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         const s2 W1 = {(short)v10, (short)v11};
         const int o = (inx & 3) + k;
         const unsigned sel = (unsigned)o | 0x0c00u | ((unsigned)(o + 1) << 16) | 0x0c000000u;
-        // this lane's J dwords: 3 (register path, DPP-shared) or 4 (LDS-DMA: a dwordx3 LDS-DMA
-        // still advances 16 B per lane in LDS, so lanes load 16 B and the quad's first 12 dwords
-        // land contiguously)
-        constexpr bool kDma = NL == 1 && LKX_DMA;
-        uint32_t joff = jrel + jbase + (uint32_t)(iny * pitch + (inx & ~3) + (kDma ? 16 : 12) * k);
-        // taps of the current window row (pa) are the previous row's lower taps (pb)
-        s2 pa[10], pb[10];
-        auto row_math = [&](const uint32_t (&rj)[11], const uint32_t (&dv)[10], const uint32_t (&cv)[10]) {
+        // this lane's 16 J bytes: the quad's first 12 dwords cover every lane's taps
+        uint32_t joff = jrel + jbase + (uint32_t)(iny * pitch + (inx & ~3) + 16 * k);
+        // union sources: lane L of piece c fills image bytes 1024c + 16L, i.e. slot sp's pair bytes wb
+        uint32_t uoff[ND];
+        {
+            const uint32_t mine = q.ubase + (uint32_t)q.v0 * rowb;
 #pragma unroll
-            for (int gi = 0; gi < 10; gi++) {
-                pb[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
-                // (J*32 - I*32) exactly as the reference's CV_DESCALE(...) - I
-                const int jd = __builtin_amdgcn_sdot2(pa[gi], W0, __builtin_amdgcn_sdot2(pb[gi], W1, (int)cv[gi], false),
-                                                      false) >> 9;
-                const float fd = (float)jd;
-                const f2 f = {(float)(int16_t)dv[gi], (float)((int)dv[gi] >> 16)};
-                acc = acc + f * fd;
-                pa[gi] = pb[gi];
+            for (int c = 0; c < ND; c++) {
+                const int P = 1024 * c + 16 * lane;
+                const int sp = P / (8 * UW), wb = P % (8 * UW);
+                uoff[c] = (uint32_t)__shfl((int)mine, sp * LPS) + (uint32_t)wb;
+            }
+        }
+        auto dma_union = [&](int b) {
+#pragma unroll
+            for (int c = 0; c < ND; c++) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)&dU[b][256 * c], 16, (int)uoff[c], 0, 0, 0);
+                uoff[c] += LKX_ROWSTEP(rowb);
             }
         };
-        if constexpr (NL == 1 && LKX_DMA) {
-            // Rows arrive by LDS-DMA (buffer_load ... lds): per row the slot's union segments of D
-            // and C (one dwordx4 per lane; the wave's lanes fill [slot][UW] in order) and each lane
-            // quad's J row segment (dwordx4 per lane, 12 of the quad's 16 dwords used).  A row's loads are issued one row ahead and
-            // retired by an explicit vmcnt(0) at the top of the next row (the compiler does not
-            // track LDS-DMA); no staging registers, no ds_write, no DPP broadcast of J.
-            uint32_t uoff = q.dlane + (uint32_t)q.v0 * rowb;
-            auto dma_union = [&](int b) {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)&dU[b][0][0], 16, (int)uoff, 0, 0, 0);
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)&dU[b][1][0], 16, (int)uoff, csoff, 0, 0);
-                uoff += LKX_ROWSTEP(rowb);
-            };
-            auto dma_j = [&](int b) {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(jrs, (lds_ptr)&dJ[b][0], 16, (int)joff, 0, 0, 0);
-                joff += LKX_ROWSTEP((uint32_t)pitch);
-            };
-            const uint32_t* lJ = &dJ[0][(lane >> 2) * 16];
-            auto read_j = [&](int b, uint32_t (&rj)[11]) {
-                const uint4 j0 = *reinterpret_cast<const uint4*>(lJ + b * 256);
-                const uint4 j1 = *reinterpret_cast<const uint4*>(lJ + b * 256 + 4);
-                const uint4 j2 = *reinterpret_cast<const uint4*>(lJ + b * 256 + 8);
-                rj[0] = j0.x; rj[1] = j0.y; rj[2] = j0.z; rj[3] = j0.w;
-                rj[4] = j1.x; rj[5] = j1.y; rj[6] = j1.z; rj[7] = j1.w;
-                rj[8] = j2.x; rj[9] = j2.y; rj[10] = j2.z;
-            };
-            const uint32_t* lD = &dU[0][0][slot * UW + q.off + k];
-            constexpr int UB = 2 * S * UW;                            // words per union buffer
-            dma_union(0);
-            dma_j(0);
-            dma_j(1);
-            lk_vmcnt0();
-            {
-                uint32_t rj[11];
-                read_j(0, rj);
+        auto dma_j = [&](int b) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(jrs, (lds_ptr)&dJ[b][0], 16, (int)joff, 0, 0, 0);
+            joff += LKX_ROWSTEP((uint32_t)pitch);
+        };
+        lds_u4v* lJ = (lds_u4v*)&dJ[0][(lane >> 2) * 16];
+        auto read_j = [&](int b, uint32_t (&rj)[11]) {
+            const v4u j0 = lJ[b * 64], j1 = lJ[b * 64 + 1], j2 = lJ[b * 64 + 2];
+            rj[0] = j0.x; rj[1] = j0.y; rj[2] = j0.z; rj[3] = j0.w;
+            rj[4] = j1.x; rj[5] = j1.y; rj[6] = j1.z; rj[7] = j1.w;
+            rj[8] = j2.x; rj[9] = j2.y; rj[10] = j2.z;
+        };
+        lds_u2v* lE = (lds_u2v*)&dU[0][2 * (slot * UW + q.off + k)];
+        // taps of the current window row (pa) are the previous row's lower taps (pb)
+        s2 pa[10], pb[10];
+        dma_union(0);
+        dma_j(0);
+        dma_j(1);
+        lk_vmcnt0();
+        {
+            uint32_t rj[11];
+            read_j(0, rj);
 #pragma unroll
-                for (int gi = 0; gi < 10; gi++) pa[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
+            for (int gi = 0; gi < 10; gi++) pa[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
+        }
+        // two rows per step with constant buffers; the taps alternate between pa and pb (no
+        // copies), and an opaque use of acc pins each row's arithmetic before the next row's wait
+        auto row = [&](int y, auto bc, s2 (&up)[10], s2 (&lo)[10]) {
+            constexpr int b = decltype(bc)::value;
+            if (y) lk_vmcnt0();                                       // union row y, J row y+1
+            // next rows' DMA right away: it writes the other buffers (union row y-1 / J row y,
+            // both consumed by the previous row), so it overlaps this row's reads and arithmetic
+            if (y + 1 < kWin) dma_union(b ^ 1);
+            if (y + 2 <= kWin) dma_j(b);
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t rj[11];
+            read_j(b ^ 1, rj);
+#pragma unroll
+            for (int gi = 0; gi < 10; gi++) {
+                const v2u dc = lE[b * UB + 4 * gi];
+                lo[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
+                // (J*32 - I*32) exactly as the reference's CV_DESCALE(...) - I
+                const int jd = __builtin_amdgcn_sdot2(up[gi], W0, __builtin_amdgcn_sdot2(lo[gi], W1, (int)dc.y, false),
+                                                      false) >> 9;
+                const float fd = (float)jd;
+                const f2 f = {(float)(int16_t)dc.x, (float)((int)dc.x >> 16)};
+                acc = acc + f * fd;
             }
-            // two rows per step with constant buffers; the taps alternate between pa and pb
-            // (no copies), and an opaque use of acc pins each row's arithmetic before the next
-            // row's wait
-            auto row = [&](int y, auto bc, s2 (&up)[10], s2 (&lo)[10]) {
-                constexpr int b = decltype(bc)::value;
-                if (y) lk_vmcnt0();                                   // union row y, J row y+1
-                uint32_t rj[11], dv[10], cv[10];
-                read_j(b ^ 1, rj);
-#pragma unroll
-                for (int gi = 0; gi < 10; gi++) {
-                    dv[gi] = lD[b * UB + 4 * gi];
-                    cv[gi] = lD[b * UB + S * UW + 4 * gi];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                if (y + 1 < kWin) dma_union(b ^ 1);
-                if (y + 2 <= kWin) dma_j(b);                          // J row y+2 over row y (read at y-1)
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int gi = 0; gi < 10; gi++) {
-                    lo[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
-                    // (J*32 - I*32) exactly as the reference's CV_DESCALE(...) - I
-                    const int jd = __builtin_amdgcn_sdot2(up[gi], W0, __builtin_amdgcn_sdot2(lo[gi], W1, (int)cv[gi], false),
-                                                          false) >> 9;
-                    const float fd = (float)jd;
-                    const f2 f = {(float)(int16_t)dv[gi], (float)((int)dv[gi] >> 16)};
-                    acc = acc + f * fd;
-                }
-                asm volatile("" : "+v"(acc));
-            };
+            asm volatile("" : "+v"(acc));
+        };
 #pragma unroll 1
-            for (int y = 0; y < kWin; y += 2) {
-                row(y, std::integral_constant<int, 0>{}, pa, pb);
-                row(y + 1, std::integral_constant<int, 1>{}, pb, pa);
-            }
-        } else {
-            {
-                const v3u m = __builtin_amdgcn_raw_buffer_load_b96(jrs, (int)joff, 0, 0);
-                u3a4 mm;
-                mm.x = m.x; mm.y = m.y; mm.z = m.z;
-                uint32_t rj[11];
-                bcast_jrow(mm, rj);
-#pragma unroll
-                for (int gi = 0; gi < 10; gi++) pa[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
-            }
-            roff = q.dlane + (uint32_t)q.v0 * rowb;
-            const uint32_t* lD0 = &lds[0][slot][q.off + k];
-            const uint32_t* lC0 = &lds[0][slot][UW + q.off + k];
-            gload();
-            lstore(0);
-            wave_lds_fence();
-#pragma unroll 2
-            for (int y = 0; y < kWin; y++) {
-                const int buf = y & 1;
-                // J row first: its use right below then waits for it alone (vmcnt retires in
-                // order), while the next union row stays in flight through this row's arithmetic
-                uint32_t rj[11];
-                joff += LKX_ROWSTEP((uint32_t)pitch);
-                const v3u jm = __builtin_amdgcn_raw_buffer_load_b96(jrs, (int)joff, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (y + 1 < kWin) gload();
-                __builtin_amdgcn_sched_barrier(0);
-                {
-                    u3a4 mm;
-                    mm.x = jm.x; mm.y = jm.y; mm.z = jm.z;
-                    bcast_jrow(mm, rj);
-                }
-                const uint32_t* ld = lD0 + buf * LBUF;
-                const uint32_t* lc = lC0 + buf * LBUF;
-                uint32_t dv[10], cv[10];
-#pragma unroll
-                for (int gi = 0; gi < 10; gi++) {
-                    dv[gi] = ld[4 * gi];
-                    cv[gi] = lc[4 * gi];
-                }
-                row_math(rj, dv, cv);
-                __builtin_amdgcn_sched_barrier(0);   // keep the staging store (and its wait) after the arithmetic
-                if (y + 1 < kWin) lstore(buf ^ 1);
-                wave_lds_fence();
-            }
+        for (int y = 0; y < kWin; y += 2) {
+            row(y, std::integral_constant<int, 0>{}, pa, pb);
+            row(y + 1, std::integral_constant<int, 1>{}, pb, pa);
         }
         if (!act) acc = f2{0.f, 0.f};
         // b = (P0+P2) + (P1+P3) across the quad; inactive quads compute values they ignore
