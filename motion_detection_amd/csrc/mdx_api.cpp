@@ -205,16 +205,28 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
                         u = std::max(u, ipx_of(r[std::min(r.size(), q + G) - 1]) - ipx_of(r[q]) + kWin);
                 return u;
             };
+            // group size 4 (less lockstep) unless 8 stages a row with fewer DMA pieces; union
+            // width = the smallest kernel shape that fits (MDX_LK_G=4/8 forces the group size)
             const int u4 = union_of(4), u8 = union_of(8);
-            if (c->lk_g == 4) {
+            auto fit = [](const int* uws, int n, int u) {
+                for (int i = 0; i < n; i++)
+                    if (uws[i] >= u) return uws[i];
+                return 0;
+            };
+            const int uw4 = fit(kLkUW4, (int)(sizeof(kLkUW4) / sizeof(int)), u4);
+            const int uw8 = fit(kLkUW8, (int)(sizeof(kLkUW8) / sizeof(int)), u8);
+            // a row's staging cost goes by LDS-DMA pieces (1 KiB, one per 64 lanes x 16 B): the
+            // wave's union row is 4 slots x uw4 or 2 slots x uw8 pairs of 8 B
+            auto pieces = [](int slots, int uw) { return (slots * uw * 8 + 1023) / 1024; };
+            const bool g4 = c->lk_g == 4 ? uw4 > 0
+                          : c->lk_g == 8 ? false
+                          : uw4 > 0 && (uw8 == 0 || pieces(4, uw4) <= pieces(2, uw8));
+            if (g4) {
                 C.G = 4;
-                C.UW = u4 <= 64 ? 64 : u4 <= 128 ? 128 : 0;
-            } else if (c->lk_g != 8 && u4 <= 64) {
-                C.G = 4;
-                C.UW = 64;
+                C.UW = uw4;
             } else {
                 C.G = 8;
-                C.UW = u8 <= 128 ? 128 : u8 <= 256 ? 256 : u8 <= 512 ? 512 : 0;
+                C.UW = uw8;
             }
             if (C.UW == 0) usable = false;
             for (const auto& r : runs) {   // each run padded to a multiple of G with -1

@@ -58,6 +58,13 @@ struct ClassLevel {
     int vlo, vhi;            // plane rows the planned grid rows' windows reach (k_lk_class range)
 };
 
+// (G, UW) shapes of the LK level kernels (mdx_lk.hip instantiates these; the host plan picks the
+// smallest UW >= a level's union span among the shapes of its G)
+#define LK_SHAPES LK_CASE(4, 48) LK_CASE(4, 56) LK_CASE(4, 64) LK_CASE(4, 72) LK_CASE(4, 80) LK_CASE(4, 96) \
+    LK_CASE(4, 128) LK_CASE(8, 80) LK_CASE(8, 112) LK_CASE(8, 128) LK_CASE(8, 256) LK_CASE(8, 512)
+constexpr int kLkUW4[] = {48, 56, 64, 72, 80, 96, 128};
+constexpr int kLkUW8[] = {80, 112, 128, 256, 512};
+
 struct ClassPlan {
     ClassLevel lv[kMaxLevels];
     long long bytes_per_pair;

@@ -228,14 +228,17 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
 //             all its groups.  So the waves are persistent and each slot, when its group retires,
 //             takes the next group from a work queue: slots of one wave run out of step, only the
 //             group-internal lockstep remains.
+// UW is the exact-fit union width (even: a 16-B load carries two pairs); the last load of a
+// slot's row and the last LDS-DMA piece of the wave's row are partial (lane-masked), so no byte
+// beyond the union is moved.
 template <int G, int UW>
 struct LkShape {
-    static constexpr int LPS = 4 * G;               // lanes per slot
-    static constexpr int S = 64 / LPS;              // slots per wave
-    static constexpr int NP = UW / (2 * LPS);       // A pass: 16-B (2-pair) loads per lane and union row
-    static constexpr int ND = S * UW * 8 / 1024;    // iterations: 1-KiB LDS-DMA pieces per union row
-    static_assert(NP >= 1 && NP * 2 * LPS == UW, "union width must be a multiple of a slot's row load");
-    static_assert(ND >= 1 && ND * 1024 == S * UW * 8, "a wave's union row must be whole LDS-DMA pieces");
+    static constexpr int LPS = 4 * G;                         // lanes per slot
+    static constexpr int S = 64 / LPS;                        // slots per wave
+    static constexpr int NP = (UW + 2 * LPS - 1) / (2 * LPS); // A pass: 16-B (2-pair) loads per lane and row
+    static constexpr int BYTES = S * UW * 8;                  // the wave's union row image
+    static constexpr int ND = (BYTES + 1023) / 1024;          // iterations: LDS-DMA pieces per row
+    static_assert(UW % 2 == 0 && UW >= kWin, "union width");
 };
 
 struct GroupGeom {
@@ -287,8 +290,9 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
 {
     using Sh = LkShape<G, UW>;
     constexpr int LPS = Sh::LPS, S = Sh::S, NP = Sh::NP;
+    constexpr int UWP = 2 * LPS * NP;                             // staged pairs per slot row
     constexpr float FLT_SCALE = 1.f / (1 << 20);
-    __shared__ __attribute__((aligned(16))) uint32_t lds[2][S][UW];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[2][S][UWP];
 
     const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
     const int nw = gridDim.x;
@@ -308,6 +312,8 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
     // rows are loaded PF ahead (this kernel has few waves' worth of VALU work to hide latency)
     constexpr int PF = 4;
     uint4 rq[PF][NP];
+    // whole loads: the staged row runs up to UWP >= UW pairs (the tail is never read by a chain;
+    // past the plane row it is the next row's data, past the slab the descriptor returns zero)
     auto gload = [&](uint4 (&rd)[NP]) {
 #pragma unroll
         for (int c = 0; c < NP; c++) {
@@ -336,7 +342,7 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
 #pragma unroll
     for (int y = 0; y < kWin; y++) {
         const int buf = y & 1;
-        const uint32_t* ld = lD0 + buf * (S * UW);
+        const uint32_t* ld = lD0 + buf * (S * UWP);
 #pragma unroll
         for (int gi = 0; gi < 10; gi++) {
             const uint32_t d = ld[4 * gi];
@@ -494,10 +500,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER
         f2 acc = {0.f, 0.f};
         if (act) iters++;
         int inx = (int)floorf(nx), iny = (int)floorf(ny);
+#ifdef LKX_FIXED   // timing-only: data-independent work (points never leave early, addresses clamped)
+        inx = min(max(inx, -kWin), L.w - 1);
+        iny = min(max(iny, -kWin), L.h - 1);
+        if (!(nx == nx)) { inx = 0; iny = 0; }
+#else
         if (act && (inx < -kWin || inx >= L.w || iny < -kWin || iny >= L.h)) {
             act = false;
             if (level == 0) status = 0;
         }
+#endif
         if (!act) { inx = 0; iny = 0; }
         const float fa = nx - (float)inx, fb = ny - (float)iny;
         int v00, v01, v10, v11;
@@ -521,14 +533,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER
             }
         }
         auto dma_union = [&](int b) {
+#if defined(LKX_NODMA) || defined(LKX_NODMA_U)   // timing-only builds: no row staging (results invalid)
+            if (uoff[0] != 0x7fffffffu) return;
+#endif
 #pragma unroll
             for (int c = 0; c < ND; c++) {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)&dU[b][256 * c], 16, (int)uoff[c], 0, 0, 0);
+                if (c < ND - 1 || 1024 * c + 16 * lane < Sh::BYTES)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)&dU[b][256 * c], 16, (int)uoff[c], 0, 0, 0);
                 uoff[c] += LKX_ROWSTEP(rowb);
             }
         };
         auto dma_j = [&](int b) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(jrs, (lds_ptr)&dJ[b][0], 16, (int)joff, 0, 0, 0);
+#if defined(LKX_NODMA) || defined(LKX_NODMA_J)
+            if (joff != 0x7fffffffu) return;
+#endif
+            // the quad's taps span 44 bytes: lanes 0-2 carry them, lane 3 stays idle
+            if (k < 3) __builtin_amdgcn_raw_ptr_buffer_load_lds(jrs, (lds_ptr)&dJ[b][0], 16, (int)joff, 0, 0, 0);
             joff += LKX_ROWSTEP((uint32_t)pitch);
         };
         lds_u4v* lJ = (lds_u4v*)&dJ[0][(lane >> 2) * 16];
@@ -706,11 +726,9 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             const int G = C.G, UW = C.UW;
             switch (G * 1000 + UW) {
-            case 4064: launch_A<4, 64>(sa, nb, b, bcls, bA, bq, l); break;
-            case 4128: launch_A<4, 128>(sa, nb, b, bcls, bA, bq, l); break;
-            case 8128: launch_A<8, 128>(sa, nb, b, bcls, bA, bq, l); break;
-            case 8256: launch_A<8, 256>(sa, nb, b, bcls, bA, bq, l); break;
-            case 8512: launch_A<8, 512>(sa, nb, b, bcls, bA, bq, l); break;
+#define LK_CASE(g, uw) case g * 1000 + uw: launch_A<g, uw>(sa, nb, b, bcls, bA, bq, l); break;
+                LK_SHAPES
+#undef LK_CASE
             default: return hipErrorInvalidValue;
             }
             if (aux) {
@@ -724,11 +742,9 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             }
             const float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             switch (C.G * 1000 + C.UW) {
-            case 4064: launch_iter<4, 64>(s, nb, b, bcls, bA, bq, l); break;
-            case 4128: launch_iter<4, 128>(s, nb, b, bcls, bA, bq, l); break;
-            case 8128: launch_iter<8, 128>(s, nb, b, bcls, bA, bq, l); break;
-            case 8256: launch_iter<8, 256>(s, nb, b, bcls, bA, bq, l); break;
-            case 8512: launch_iter<8, 512>(s, nb, b, bcls, bA, bq, l); break;
+#define LK_CASE(g, uw) case g * 1000 + uw: launch_iter<g, uw>(s, nb, b, bcls, bA, bq, l); break;
+                LK_SHAPES
+#undef LK_CASE
             default: return hipErrorInvalidValue;
             }
         }
