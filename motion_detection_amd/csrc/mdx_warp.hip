@@ -11,25 +11,35 @@
 //   sx = X >> 5, fx = X & 31, ...;  out = (sum v_i * w_i + 2^14) >> 15 with w_i from (fx, fy)
 //   mask = |out - gray2| > thresh ? 255 : 0
 //
-// Fast path (affine M, bw0 == 64, full-width tile over dword-aligned buffers, the tile's source
-// footprint small): one 256-thread workgroup per 64 x 128 destination tile (= one reference block
-// column, eight block rows).  Lane l of wave w owns the 4 columns x0 + 4*(l & 15) .. +3 of rows
-// y0 + 32w + 4i + (l >> 4), i = 0..7, so gray2 loads / mask stores are dwords, 64 contiguous bytes
-// per row.  Wave 0 computes the footprint; the workgroup stages it.
-//   * The tile's source footprint (exact: X, Y are monotone in x and y for affine M, so the
-//     four corners bound it) is staged once into LDS as raw bytes with ds_write_b128, zero
-//     outside the image (= BORDER_CONSTANT 0 per tap), row pitch kSP = 96 B; taps are 4 byte
-//     reads with immediate offsets (0, 1, 96, 97).
-//   * Per column, M0*x1 and M3*x1 stay in registers (4 columns per lane); per row, X0 and Y0 come
-//     from a 128-entry LDS table.  Per pixel: two FP64 adds and two multiply-adds with the magic
-//     constant 1.5*2^52 - 32*origin, whose low word is cvRound(.) relative to the staged origin
-//     (round-half-even, exact for |X| < 2^30, checked per tile).  When 32/M8 is a power of two the
-//     multiply is exact and fuses with the rounding add into one FMA.
-//   * Bilinear: w = (32-fx)(32-fy)*32 ... factorises exactly into three v_dot2_u32_u16 on taps
-//     loaded straight into u16 halves (ds_read_u8_d16/_hi): q0 = dot(v00 v10, 32-fy fy),
-//     q1 = dot(v01 v11, .), out = (dot(q0 q1, 32-fx fx) + 512) >> 10.
-//   * |out - g2| + (32767 - thresh) has bit 15 set iff the pixel is moving (v_sad_u16); v_perm's
-//     sign-replicating selectors turn four such bits into the four 0x00/0xff mask bytes.
+// Fast path (affine M, bw0 == 64, dword-aligned buffers, the tile's source footprint small): one
+// 256-thread workgroup per 128 x 64 destination tile (two reference block columns; 64 rows
+// measured best: 32 doubles the per-tile setup, 128 halves the workgroups a CU holds).  Lane l of
+// wave w owns the 4 columns x0 + 4*(l & 31) .. +3 of rows y0 + 8i + 2w + (l >> 5), i = 0..7: a
+// half-wave is one tile row, so gray2 loads / mask stores are dwords, 128 contiguous bytes.
+//   * Footprint: X, Y are monotone in x and y inside a reference block for affine M, so the eight
+//     block corners bound the tile's taps exactly.  It is staged once into LDS as raw bytes
+//     (16-B loads, ds_write_b128), zero outside the image (= BORDER_CONSTANT 0 per tap), at a row
+//     pitch of 256 B.
+//   * Coordinates, per pixel: one FP64 add (per-row X0 from an LDS table + per-column M0*x1 in
+//     registers) and one FMA with the magic constant 1.5*2^52 - 32*origin per axis, whose low word
+//     is cvRound(32*(...)) - 32*origin (round-half-even, exact for |X| < 2^30, checked per tile).
+//     When 32/M8 is not a power of two the product (...)*Wd is rounded first, as the reference
+//     does, and the add only rounds it to an integer.
+//   * Shifted left by 3, byte 1 of each low word is the staged source column (row) and bits 3..7
+//     are 8*fx (8*fy): the tap address (row << 8 | col) is ONE v_perm, and 8*f indexes a 32-entry
+//     LDS weight table (entry f: wy = (32-f, f), wx = 64*(32-f, f)).
+//   * Taps: four byte reads per pixel, c0 = (v00, v01), c1 = (v10, v11) as u16 halves.  Vertical
+//     with two packed u16 ops (op_sel splats the weight halves), q = c0*(32-fy) + c1*fy =
+//     (q0, q1) <= 8160; horizontal with one v_dot2_u32_u16: s = 64*(q0 (32-fx) + q1 fx) + 32.
+//   * Threshold without the >> 10: out = (S + 512) >> 10 with S = (s - 32)/64, and
+//     |out - g| > t  <=>  |s - 65536 g| >= 65536 t + 32800 (exact).
+//     v_sad_u32(s, g << 16, 2^31 - 65536 t - 32800) sets bit 31 iff the pixel moves (g << 16 is
+//     one v_perm of the gray2 dword); v_perm's sign-replicating selectors turn the four flags
+//     into the four 0x00/0xff mask bytes.
+//   * gray2 loads / mask stores go through buffer descriptors: lanes past the right edge get an
+//     out-of-range offset and rows past the band fall outside the mask descriptor, so the row
+//     loop is branch-free.  ~17 VALU per pixel (4 of them FP64), vs ~23 for the 64x128-tile
+//     design before it (rocprofv3 SQ_INSTS_VALU).
 // Everything else (perspective M, small frames, huge or far-away footprints) takes the general
 // per-pixel path, exact for any input.
 #include "mdx_internal.h"
@@ -38,22 +48,19 @@
 
 namespace mdx {
 
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
 
-
-constexpr int kWTile = 64;              // tile = one reference block column (bw0 = 64)
+constexpr int kTW = 128;     // tile width: two reference block columns (bw0 = 64)
+constexpr int kBW = 64;      // reference block width of the fast path
 #ifndef WX_TH
-#define WX_TH 128
+#define WX_TH 64
 #endif
-constexpr int kHTile = WX_TH;           // 16 * reference block rows (default 8 block rows)
-#ifndef WX_SP
-#define WX_SP 96
+constexpr int kTH = WX_TH;   // tile rows
+constexpr int kSP = 256;     // staged row pitch: tap address = (row << 8) | col, one v_perm
+#ifndef WX_SH
+#define WX_SH (WX_TH + 12)
 #endif
-// staged row pitch, bytes.  96 (24 dwords) leaves some 2-way bank conflicts between the two tap
-// rows a half-wave reads, but 15 KiB of LDS per workgroup lets 8 workgroups share a CU, which
-// hides the staging latency better than the conflict-free 192 (measured 258 vs 284 us, 4K x32).
-constexpr int kSP = WX_SP;
-constexpr int kSH = 136;                // staged rows (tile height + rotation/scale margin)
+constexpr int kSH = WX_SH;   // staged rows (tile height + scale/rotation margin)
 
 __device__ __forceinline__ int clamp_int_from_double(double v)
 {
@@ -97,20 +104,26 @@ __device__ __forceinline__ uint8_t warp_px_general(const double* M, const uint8_
 }
 
 struct TileInfo {
+    double wd;         // 32 / M8 (affine: W = M8 everywhere), 0 when M8 == 0
     int fast;          // 1: fast path usable for this tile
     int sxa, sya;      // staged origin (sxa multiple of 16)
-    int sw, sh, lp;    // staged width (bytes), height (rows), LDS row pitch
+    int sw, sh;        // staged width (bytes), height (rows)
 };
 
-// Bounds of the tile's taps, computed on lanes 0..3 (one corner each) with the reference
-// arithmetic; fast = every |X|, |Y| < 2^30 (no clamp, magic rounding exact) and the footprint fits.
-__device__ TileInfo tile_info(const double* M, double Wd, int x0, int y0, int w, int yend, int lane)
+// Bounds of the tile's taps, from the reference arithmetic at the corners of its (one or two)
+// reference blocks, one corner per lane 0..7; fast = every |X|, |Y| < 2^30 (no clamp, magic
+// rounding exact) and the footprint fits the staging buffer.
+__device__ TileInfo tile_info(const double* M, int x0, int y0, int w, int yend, int lane)
 {
-    const int cxl = min(kWTile - 1, w - 1 - x0), cyl = min(kHTile - 1, yend - 1 - y0);
+    const double Wd = M[8] != 0.0 ? 32.0 / M[8] : 0.0;
+    const int nb = (x0 + kBW < w) ? 2 : 1;                       // reference blocks in the tile
+    const int b = ((lane >> 2) & 1) < nb ? ((lane >> 2) & 1) : 0;
+    const int xb = x0 + kBW * b;
+    const int cxl = min(kBW - 1, w - 1 - xb), cyl = min(kTH - 1, yend - 1 - y0);
     const int c = lane & 3;
     const int x1 = (c & 1) ? cxl : 0, y = y0 + ((c & 2) ? cyl : 0);
-    const double X0 = M[0] * x0 + M[1] * y + M[2];
-    const double Y0 = M[3] * x0 + M[4] * y + M[5];
+    const double X0 = M[0] * xb + M[1] * y + M[2];
+    const double Y0 = M[3] * xb + M[4] * y + M[5];
     const double px = (X0 + M[0] * x1) * Wd, py = (Y0 + M[3] * x1) * Wd;
     const double lim = 1073741824.0;   // 2^30
     int ok = (px > -lim && px < lim && py > -lim && py < lim) ? 1 : 0;
@@ -121,120 +134,125 @@ __device__ TileInfo tile_info(const double* M, double Wd, int x0, int y0, int w,
     }
     int sx_lo = sx, sx_hi = sx, sy_lo = sy, sy_hi = sy;
 #pragma unroll
-    for (int m = 1; m <= 2; m <<= 1) {
-        sx_lo = min(sx_lo, __shfl_xor(sx_lo, m, 4));
-        sx_hi = max(sx_hi, __shfl_xor(sx_hi, m, 4));
-        sy_lo = min(sy_lo, __shfl_xor(sy_lo, m, 4));
-        sy_hi = max(sy_hi, __shfl_xor(sy_hi, m, 4));
-        ok = min(ok, __shfl_xor(ok, m, 4));
+    for (int m = 1; m <= 4; m <<= 1) {
+        sx_lo = min(sx_lo, __shfl_xor(sx_lo, m, 8));
+        sx_hi = max(sx_hi, __shfl_xor(sx_hi, m, 8));
+        sy_lo = min(sy_lo, __shfl_xor(sy_lo, m, 8));
+        sy_hi = max(sy_hi, __shfl_xor(sy_hi, m, 8));
+        ok = min(ok, __shfl_xor(ok, m, 8));
     }
     TileInfo t;
+    t.wd = Wd;
     t.sxa = __builtin_amdgcn_readfirstlane(sx_lo) & ~15;
     t.sya = __builtin_amdgcn_readfirstlane(sy_lo);
     const int sxb = __builtin_amdgcn_readfirstlane(sx_hi), syb = __builtin_amdgcn_readfirstlane(sy_hi);
     t.sw = sxb - t.sxa + 2;                    // bytes: columns sxa .. sxb + 1
     t.sh = syb - t.sya + 2;                    // rows sya .. syb + 1
-    t.lp = kSP;
     t.fast = __builtin_amdgcn_readfirstlane(ok) && t.sw > 0 && t.sh > 0 && t.sw <= kSP && t.sh <= kSH;
     return t;
 }
 
-typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
-// LDS pointers stay 32-bit (address space 3) through the inlined helper
+// LDS pointers stay 32-bit (address space 3) through the inlined helpers
 typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
 typedef double d2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const d2v lds_d2;
 
-// Fast-path rows of one lane: 4 columns x nrows rows (every 4th tile row from r0).  The tile is
-// full width and the buffers dword-aligned (checked by the caller), so loads/stores are dwords.
-template <bool POW2>
-__device__ __forceinline__ void warp_rows(lds_d2* s_xy, lds_u8* s_src, int r0, int nrows, int y0, int xs,
-                                          const uint8_t* g2p, int g2_pitch, uint8_t* mp, int w, const double* tx,
+// raw buffer descriptor over [base, base + bytes): out-of-range loads return 0 and stores are
+// dropped, which is how lanes past the right edge and rows past the band go quiet.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, long long bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                             (int)min(bytes, (long long)0x7fffffff), 0x00020000);
+}
+
+// Fast-path rows of one lane: 4 columns x 8 rows (tile rows r0 + 8i).  xyp points at this lane's
+// (X0, Y0) of row r0 and block; tab8 at the weight table (entry f at byte 8f: (32-f, f), then
+// 64*(32-f, f)); src_base is the staged footprint.  g2 / mask go through buffer descriptors whose
+// per-lane offsets are out of range for idle lanes; ROWCHK (partial tiles) sends rows past the
+// band to row r0's coordinates so every tap stays inside the footprint.
+template <bool POW2, bool ROWCHK>
+__device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t src_base, int nvalid,
+                                          __amdgpu_buffer_rsrc_t g2rs, uint32_t g2off, int g2s,
+                                          __amdgpu_buffer_rsrc_t mrs, uint32_t moff, int ms, const double* tx,
                                           const double* ty, double Wd, double mX, double mY, uint32_t bias)
 {
-    const uint8_t* g2r = g2p + (long long)(y0 + r0) * g2_pitch + xs;
-    uint8_t* mr = mp + (long long)(y0 + r0) * w + xs;   // mp: mask row 0 of the pair's band, shifted by -row0
-    const long long g2s = 4LL * g2_pitch, ms = 4LL * w;
-    for (int i = 0; i < nrows; i++, g2r += g2s, mr += ms) {
-        const d2v xy = s_xy[r0 + 4 * i];
-#ifndef WX_NO_G2   // WX_*: timing-only builds (scripts/warp_variants.sh), results invalid
-        const uint32_t G = *reinterpret_cast<const uint32_t*>(g2r);
-#else
-        const uint32_t G = (uint32_t)i * 0x01010101u;
-#endif
-        uint32_t wxs[4], wys[4], c0s[4], c1s[4];
+    uint32_t G[kTH / 8];
+#pragma unroll
+    for (int i = 0; i < kTH / 8; i++) G[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * g2s, 0);
+#pragma unroll
+    for (int i = 0; i < kTH / 8; i++) {
+        const d2v xy = xyp[ROWCHK ? (i < nvalid ? 16 * i : 0) : 16 * i];   // rows are 2 blocks x 16 B apart
+        uint32_t xs_[4], ys_[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const double ax = xy.x + tx[k], ay = xy.y + ty[k];
             double rx, ry;
-            if (POW2) {
+            if (POW2) {                                   // (X0 + M0*x1) * Wd exact: one rounding
                 rx = __builtin_fma(ax, Wd, mX);
                 ry = __builtin_fma(ay, Wd, mY);
-            } else {
+            } else {                                      // round the product, then to integer
                 rx = ax * Wd + mX;
                 ry = ay * Wd + mY;
             }
-            const uint32_t X = (uint32_t)__double2loint(rx);   // cvRound((...)*Wd) - 32*sxa, >= 0
-            const uint32_t Y = (uint32_t)__double2loint(ry);
-            const uint32_t fx = X & 31u, fy = Y & 31u;
-            const uint32_t off = __umul24(Y >> 5, (uint32_t)kSP) + (X >> 5);   // v_mad_u32_u24
-            wxs[k] = fx * 65535u + 32u;                 // u16 (32 - fx, fx)
-            wys[k] = fy * 65535u + 32u;                 // u16 (32 - fy, fy)
-#ifndef WX_NO_TAPS
-#ifdef WX_D16
-            // taps straight into u16 halves: c0 = (v00, v10), c1 = (v01, v11)
-            const uint32_t a = (uint32_t)(uintptr_t)(s_src + off);
-            uint32_t c0, c1;
-            asm volatile("ds_read_u8_d16 %0, %2\n\t"
-                         "ds_read_u8_d16_hi %0, %2 offset:%3\n\t"
-                         "ds_read_u8_d16 %1, %2 offset:1\n\t"
-                         "ds_read_u8_d16_hi %1, %2 offset:%4"
-                         : "=&v"(c0), "=&v"(c1) : "v"(a), "i"(kSP), "i"(kSP + 1));
-            c0s[k] = c0;
-            c1s[k] = c1;
-#else
-            c0s[k] = (uint32_t)s_src[off] | ((uint32_t)s_src[off + kSP] << 16);
-            c1s[k] = (uint32_t)s_src[off + 1] | ((uint32_t)s_src[off + kSP + 1] << 16);
-#endif
-#else
-            c0s[k] = (off & 255) | (((off >> 3) & 255) << 16);
-            c1s[k] = ((off >> 5) & 255) | (((off >> 7) & 255) << 16);
-#endif
+            xs_[k] = (uint32_t)__double2loint(rx);        // X - 32 * sxa
+            ys_[k] = (uint32_t)__double2loint(ry);        // Y - 32 * sya
         }
-#if defined(WX_D16) && !defined(WX_NO_TAPS)
-        // the asm loads are invisible to the compiler's waitcnt pass: wait here, and make every
-        // tap register an operand so no use can be scheduled above the wait
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(c0s[0]), "+v"(c0s[1]), "+v"(c0s[2]), "+v"(c0s[3]), "+v"(c1s[0]), "+v"(c1s[1]),
-                       "+v"(c1s[2]), "+v"(c1s[3])
-                     :
-                     : "memory");
-#endif
-        uint32_t e4[4];
+        uint32_t ad[4], wys[4], wxs[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            // vertical then horizontal: sum_i v_i (32-fx|fx)(32-fy|fy), exact in integers
-            const uint32_t q0 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, c0s[k]), __builtin_bit_cast(u16x2v, wys[k]), 0u, false);
-            const uint32_t q1 = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, c1s[k]), __builtin_bit_cast(u16x2v, wys[k]), 0u, false);
-            const uint32_t sv = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, q0 | (q1 << 16)),
-                                                       __builtin_bit_cast(u16x2v, wxs[k]), 512u, false);
-            const uint32_t v = sv >> 10;
-            // |v - g| + 32767 - thresh: bit 15 set iff |v - g| > thresh (value < 2^16)
-            e4[k] = __builtin_amdgcn_sad_u16(v, (G >> (8 * k)) & 255u, bias);
-        }
-        // v_perm selectors 8 / 10 replicate bit 15 / bit 47 of {src0:src1}: 0xff or 0x00 bytes
-        const uint32_t e01 = e4[0] | (e4[1] << 16), e23 = e4[2] | (e4[3] << 16);
-        const uint32_t out = __builtin_amdgcn_perm(e23, e01, 0x0b0a0908u);
-#ifndef WX_NO_STORE
-        *reinterpret_cast<uint32_t*>(mr) = out;
+#ifdef WX_DIRECT
+            // weights computed: (32 - fy, fy) and 64 * (32 - fx, fx)
+            ad[k] = src_base + ((ys_[k] >> 5) << 8 | (xs_[k] >> 5));
+            wys[k] = (ys_[k] & 31u) * 65535u + 32u;
+            wxs[k] = (xs_[k] & 31u) * (64u * 65535u) + 2048u;
 #else
-        if (out == bias) *reinterpret_cast<uint32_t*>(mr) = out;   // runtime-false: keeps the work
+            // 8X: byte 1 is the staged column (row), bits 3..7 index the 8-B weight table
+            const uint32_t lx = xs_[k] << 3, ly = ys_[k] << 3;
+            ad[k] = src_base + __builtin_amdgcn_perm(ly, lx, 0x0c0c0501u);   // (row << 8) | col
+            wys[k] = *(lds_u32*)(tab8 + (ly & 0xf8u));       // (32 - fy, fy)
+            wxs[k] = *(lds_u32*)(tab8 + (lx & 0xf8u) + 4);   // 64 * (32 - fx, fx)
 #endif
+        }
+        // taps: four byte reads per pixel, c0 = (v00, v01), c1 = (v10, v11) as u16 halves.
+        // (ds_read_*_d16_hi does not preserve the low half on gfx950 with SRAM ECC, and unaligned
+        // ds_read_u16 is correct but ~4x slower here.)
+        uint32_t c0s[4], c1s[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            lds_u8* p = (lds_u8*)(uintptr_t)ad[k];
+            c0s[k] = (uint32_t)p[0] | ((uint32_t)p[1] << 16);
+            c1s[k] = (uint32_t)p[kSP] | ((uint32_t)p[kSP + 1] << 16);
+        }
+        uint32_t e[4];
+#ifdef WX_DEBUG_VAL
+        uint32_t sv_[4];
+#endif
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u16x2v c0 = __builtin_bit_cast(u16x2v, c0s[k]), c1 = __builtin_bit_cast(u16x2v, c1s[k]);
+            const u16x2v wy = __builtin_bit_cast(u16x2v, wys[k]);
+            const u16x2v q = c0 * wy.xx + c1 * wy.yy;     // (q0, q1): vertical, exact in u16
+            const uint32_t s = __builtin_amdgcn_udot2(q, __builtin_bit_cast(u16x2v, wxs[k]), 32u, false);
+            const uint32_t g16 = __builtin_amdgcn_perm(0u, G[i], 0x0c000c0cu | ((uint32_t)k << 16));   // g_k << 16
+            asm("v_sad_u32 %0, %1, %2, %3" : "=v"(e[k]) : "v"(s), "v"(g16), "s"(bias));   // bit 31: moving
+#ifdef WX_DEBUG_VAL
+            sv_[k] = s;
+#endif
+        }
+        // v_perm selectors 9 / 11 replicate bit 31 of src1 / src0: 0xff or 0x00 bytes
+#ifndef WX_DEBUG_VAL
+        const uint32_t out = __builtin_amdgcn_perm(e[1], e[0], 0x0c0c0b09u) | __builtin_amdgcn_perm(e[3], e[2], 0x0b090c0cu);
+#else   // debug build: the warped values instead of the mask
+        uint32_t out = 0;
+        for (int k = 0; k < 4; k++) out |= ((sv_[k] + 32736u) >> 16) << (8 * k);
+#endif
+        __builtin_amdgcn_raw_buffer_store_b32(out, mrs, (int)moff, i * ms, 0);
     }
 }
 
 // grid: x -> tile column, y -> tile row of the band [row0, row1), z -> pair.  256 threads; lane l
-// of wave q owns columns x0 + 4*(l & 15) .. +3 of tile rows 32q + (l >> 4) + 4i, i = 0..7.  The
+// of wave q owns columns x0 + 4*(l & 31) .. +3 of tile rows 2q + (l >> 5) + 8i, i = 0..7.  The
 // reference's blocking depends on the full height only through bw0, and each pixel's arithmetic
 // on (x, y) only, so a band is exactly the full frame's rows.
 __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
@@ -243,7 +261,8 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
                                                    uint8_t* __restrict__ mask, long long mask_stride, int thresh,
                                                    int vec_ok, int row0, int row1)
 {
-    __shared__ __attribute__((aligned(16))) double s_xy[kHTile][2];    // (X0, Y0) per tile row
+    __shared__ __attribute__((aligned(16))) uint32_t s_tab[64];             // weight table
+    __shared__ __attribute__((aligned(16))) double s_xy[kTH][2][2];         // (X0, Y0) per row, block
     __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
     __shared__ TileInfo s_info;
 
@@ -259,19 +278,18 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     }
     const int pair = bid / (nbx * nby), tile = bid - pair * (nbx * nby);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int x0 = (tile % nbx) * kWTile, y0 = row0 + (tile / nbx) * kHTile;
-    const int cq = lane & 15, rr = lane >> 4;
+    const int x0 = (tile % nbx) * kTW, y0 = row0 + (tile / nbx) * kTH;
+    const int cq = lane & 31;
     const int xs = x0 + 4 * cq;                     // this lane's 4 columns
-    const int r0 = (kHTile / 4) * wave + rr;        // this lane's first tile row
-    const int nrows = max(0, min(kHTile / 16, (row1 - y0 - r0 + 3) >> 2));
+    const int r0 = 2 * wave + (lane >> 5);          // this lane's first tile row (then every 8th)
     const uint8_t* g2p = g2 + (long long)pair * g2_stride;
     uint8_t* mp = mask + (long long)pair * mask_stride - (long long)row0 * w;   // indexed by frame row
 
     const PairFit& f = fits[pair];
     if (f.fit_status != 0) {   // no fit: the reference produces no mask; ours is all zero
         const int nx = max(0, min(4, w - xs));
-        for (int i = 0; i < nrows; i++) {
-            uint8_t* m = mp + (long long)(y0 + r0 + 4 * i) * w + xs;
+        for (int r = r0; r < kTH && y0 + r < row1; r += 8) {
+            uint8_t* m = mp + (long long)(y0 + r) * w + xs;
             for (int k = 0; k < nx; k++) m[k] = 0;
         }
         return;
@@ -281,12 +299,11 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     for (int k = 0; k < 9; k++) M[k] = f.Hinv[k];
     const uint8_t* src = g1 + (long long)pair * g1_stride;
     const bool affine = (M[6] == 0.0) && (M[7] == 0.0);
-    const double Wd = M[8] != 0.0 ? 32.0 / M[8] : 0.0;   // affine: W = M8 everywhere
-    // fast path only for full-width tiles over dword-aligned rows (uniform per workgroup)
-    const bool try_fast = affine && bw0 == kWTile && vec_ok && x0 + kWTile <= w;
+    // fast path only over dword-aligned rows with reference blocks of 64 (uniform per workgroup)
+    const bool try_fast = affine && bw0 == kBW && vec_ok;
 
     if (try_fast && wave == 0) {
-        const TileInfo t = tile_info(M, Wd, x0, y0, w, row1, lane);
+        const TileInfo t = tile_info(M, x0, y0, w, row1, lane);
         if (lane == 0) s_info = t;
     }
     if (try_fast) __syncthreads();
@@ -294,8 +311,8 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     if (!try_fast || !t.fast) {
         // ---- general path: per pixel, global gathers
         const int nx = max(0, min(4, w - xs));
-        for (int i = 0; i < nrows; i++) {
-            const int y = y0 + r0 + 4 * i;
+        for (int r = r0; r < kTH && y0 + r < row1; r += 8) {
+            const int y = y0 + r;
             const uint8_t* g2r = g2p + (long long)y * g2_pitch + xs;
             uint8_t* m = mp + (long long)y * w + xs;
             for (int k = 0; k < nx; k++) m[k] = warp_px_general(M, src, g1_pitch, w, h, xs + k, y, bw0, g2r[k], thresh);
@@ -303,11 +320,15 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
         return;
     }
 
-    // ---- fast path: per-row X0/Y0, then stage the footprint (rows sya.., 16-B chunks from sxa)
-    if (tid < kHTile) {
-        const int y = y0 + tid;
-        s_xy[tid][0] = M[0] * x0 + M[1] * y + M[2];
-        s_xy[tid][1] = M[3] * x0 + M[4] * y + M[5];
+    // ---- fast path: weight table, per-row X0/Y0 of both blocks, then stage the footprint
+    if (tid < 32) {
+        s_tab[2 * tid] = (uint32_t)(32 - tid) | ((uint32_t)tid << 16);
+        s_tab[2 * tid + 1] = (uint32_t)(64 * (32 - tid)) | ((uint32_t)(64 * tid) << 16);
+    }
+    if (tid < 2 * kTH) {
+        const int r = tid >> 1, b = tid & 1, y = y0 + r, xb = x0 + kBW * b;
+        s_xy[r][b][0] = M[0] * xb + M[1] * y + M[2];
+        s_xy[r][b][1] = M[3] * xb + M[4] * y + M[5];
     }
     {
         const int nch = (t.sw + 15) >> 4;                 // <= kSP / 16
@@ -319,7 +340,7 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
             for (int r = ro; r < t.sh; r += rpp) {
                 const int sy = t.sya + r;
                 uint4 v;
-#ifdef WX_NO_STAGE
+#ifdef WX_NO_STAGE   // WX_*: timing-only builds (scripts/warp_variants.sh), results invalid
                 if (true) {
                     v = make_uint4(sy, sx, r, ch);
 #else
@@ -342,26 +363,47 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
         }
     }
     __syncthreads();
-    if (nrows == 0) return;
 
-    const double magic = 6755399441055744.0;                 // 1.5 * 2^52
+    // lanes past the right edge compute on a valid column of block 0 and store nothing
+    const bool col_ok = xs < w;
+    const int cqe = col_ok ? cq : (cq & 15);
+    const int blk = cqe >> 4, x1b = 4 * (cqe & 15);
+    const double Wd = t.wd;                                  // computed once, by wave 0
+    const double magic = 6755399441055744.0;                 // 1.5 * 2^52: ulp 1
     const double mX = magic - 32.0 * t.sxa, mY = magic - 32.0 * t.sya;
     // 32/M8 a power of two -> (X0 + M0*x1) * Wd is exact and fuses with the rounding add
     const bool pow2 = Wd != 0.0 && (__double_as_longlong(Wd) & 0x000fffffffffffffLL) == 0;
-    const uint32_t bias = 32767u - (uint32_t)thresh;
+    const int tc = min(max(thresh, -1), 255);                // t < 0: all moving; t >= 255: none
+    const uint32_t bias = 0x80000000u - (uint32_t)(65536 * tc + 32800);
     double tx[4], ty[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        tx[k] = M[0] * (4 * cq + k);
-        ty[k] = M[3] * (4 * cq + k);
+        tx[k] = M[0] * (x1b + k);
+        ty[k] = M[3] * (x1b + k);
         asm volatile("" : "+v"(tx[k]), "+v"(ty[k]));   // keep in registers (no per-row rematerialisation)
     }
-    lds_d2* xyp = (lds_d2*)(&s_xy[0][0]);
-    lds_u8* srcp = (lds_u8*)(&s_src[0]);
-    if (pow2)
-        warp_rows<true>(xyp, srcp, r0, nrows, y0, xs, g2p, g2_pitch, mp, w, tx, ty, Wd, mX, mY, bias);
-    else
-        warp_rows<false>(xyp, srcp, r0, nrows, y0, xs, g2p, g2_pitch, mp, w, tx, ty, Wd, mX, mY, bias);
+    lds_d2* xyp = (lds_d2*)(&s_xy[r0][blk][0]);
+    lds_u8* tabp = (lds_u8*)(&s_tab[0]);
+    const uint32_t src_base = (uint32_t)(uintptr_t)(lds_u8*)(&s_src[0]);
+    // gray2 rows of this pair; mask rows [0, row1) of the frame (stores past the band drop)
+    const __amdgpu_buffer_rsrc_t g2rs = buf_rsrc(g2p, (long long)h * g2_pitch);
+    const __amdgpu_buffer_rsrc_t mrs = buf_rsrc(mp, (long long)row1 * w);
+    const uint32_t OOB = 0x80000000u;
+    const uint32_t g2off = col_ok ? (uint32_t)((y0 + r0) * g2_pitch + xs) : OOB;
+    const uint32_t moff = col_ok ? (uint32_t)((y0 + r0) * w + xs) : OOB;
+    const int nvalid = (row1 - y0 - r0 + 7) >> 3;            // rows r0 + 8i inside the band: i < nvalid
+    const bool rowchk = y0 + kTH > row1;
+    if (pow2) {
+        if (!rowchk)
+            warp_rows<true, false>(xyp, tabp, src_base, nvalid, g2rs, g2off, 8 * g2_pitch, mrs, moff, 8 * w, tx, ty, Wd,
+                                   mX, mY, bias);
+        else
+            warp_rows<true, true>(xyp, tabp, src_base, nvalid, g2rs, g2off, 8 * g2_pitch, mrs, moff, 8 * w, tx, ty, Wd,
+                                  mX, mY, bias);
+    } else {
+        warp_rows<false, true>(xyp, tabp, src_base, nvalid, g2rs, g2off, 8 * g2_pitch, mrs, moff, 8 * w, tx, ty, Wd, mX,
+                               mY, bias);
+    }
 }
 
 hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,
@@ -375,7 +417,7 @@ hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long lo
     // dword loads of gray2 / stores of the mask need 4-B aligned rows
     const int vec_ok = ((uintptr_t)g2 % 4 == 0) && g2_stride % 4 == 0 && g2_pitch % 4 == 0 &&
                        ((uintptr_t)mask % 4 == 0) && mask_stride % 4 == 0 && w % 4 == 0;
-    const dim3 grid((w + kWTile - 1) / kWTile, (row1 - row0 + kHTile - 1) / kHTile, batch);
+    const dim3 grid((w + kTW - 1) / kTW, (row1 - row0 + kTH - 1) / kTH, batch);
     hipLaunchKernelGGL(k_warp_diff, grid, dim3(256), 0, s, g1, g1_stride, g1_pitch, g2, g2_stride, g2_pitch, w, h, bw0,
                        fits, mask, mask_stride, thresh, vec_ok, row0, row1);
     return hipGetLastError();

@@ -1,0 +1,100 @@
+"""GPU parity of the fused warp + absdiff + threshold kernel (rows A8-A10) over the geometries
+and thresholds its fast path special-cases, through the C-ABI entry `mdx_warp_diff_dev`.
+
+Reference: common/src/optical_flow_calculator.cpp:124-127 (warpPerspective, absdiff,
+threshold(., 190, 255, THRESH_BINARY)).  The checker is the oracle's warp_perspective
+(OpenCV 2.4 WarpPerspectiveInvoker restated) + numpy absdiff/threshold; the bar is bit-exact.
+
+Cases: frame widths that are / are not multiples of the 128-px tile (partial reference blocks),
+band-edge rows, homographies whose 1/32-px coordinates fall exactly on rounding ties
+(translation by 1/64 px), flips (M0 < 0), zoom in/out (footprint larger than the LDS staging
+buffer -> general path), projective and singular M, and thresholds -1, 0, 10, 190, 254, 255, 300.
+"""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _rot(deg, s=1.0, tx=0.0, ty=0.0, cx=0.0, cy=0.0):
+    c, si = math.cos(math.radians(deg)) * s, math.sin(math.radians(deg)) * s
+    # rotate/scale about (cx, cy), then translate
+    return np.array([[c, -si, cx - c * cx + si * cy + tx], [si, c, cy - si * cx - c * cy + ty], [0.0, 0.0, 1.0]])
+
+
+def _H(kind, w, h, Ht):
+    return {
+        "true": Ht,
+        "identity": np.eye(3),
+        "tie_translation": np.array([[1.0, 0.0, 1.0 / 64], [0.0, 1.0, -3.0 / 64], [0.0, 0.0, 1.0]]),
+        "tie_scale_half": np.array([[0.5, 0.0, 0.25 / 32], [0.0, 2.0, 0.0], [0.0, 0.0, 1.0]]),
+        "rot5": _rot(5.0, 1.0, 2.3, -1.1, w / 2, h / 2),
+        "flip_x": np.array([[-1.0, 0.0, w - 1.0 + 0.3], [0.0, 1.0, 0.7], [0.0, 0.0, 1.0]]),
+        "zoom_in": _rot(0.0, 1.6, 0.0, 0.0, w / 2, h / 2),
+        "zoom_out": _rot(0.0, 0.6, 0.0, 0.0, w / 2, h / 2),
+        "far_away": np.array([[1.0, 0.0, -5000.0], [0.0, 1.0, 12.0], [0.0, 0.0, 1.0]]),
+        "m8_not_pow2": np.array([[1.01, 0.002, 3.2], [-0.003, 0.99, -1.7], [0.0, 0.0, 1.3]]),
+        "projective": np.array([[1.002, 0.013, -2.5], [-0.011, 0.995, 1.75], [2.1e-5, -1.3e-5, 1.0]]),
+        "singular": np.zeros((3, 3)),
+    }[kind]
+
+
+@pytest.fixture(scope="module")
+def wctx(mdx):
+    c = mdx.Context(0, 3840, 2160, 1)
+    yield c
+    c.close()
+
+
+def _run(mdx, ctx, oracle, g1, g2, Hs, thresh):
+    B, h, w = g1.shape
+    Hb = np.ascontiguousarray(np.stack(Hs).astype(np.float64))
+    ctx.set_params(thresh=thresh)
+    d1, d2, dH, dM = (ctx.dev_alloc(x) for x in (g1.nbytes, g2.nbytes, Hb.nbytes, B * w * h))
+    try:
+        ctx.h2d(d1, g1); ctx.h2d(d2, g2); ctx.h2d(dH, Hb)
+        ctx.warp_diff_dev(B, d1, d2, w, h, w, w * h, dH, dM)
+        ctx.sync()
+        out = np.empty((B, h, w), np.uint8)
+        ctx.d2h(out, dM)
+    finally:
+        ctx.set_params(thresh=190)
+        for p in (d1, d2, dH, dM):
+            ctx.dev_free(p)
+    for i in range(B):
+        warped = oracle.warp_perspective(g1[i], oracle.invert3x3(Hb[i]), nthreads=8)
+        ref = np.where(np.abs(warped.astype(np.int16) - g2[i].astype(np.int16)) > thresh, 255, 0).astype(np.uint8)
+        bad = np.argwhere(out[i] != ref)
+        assert bad.size == 0, f"pair {i}: {len(bad)} mask pixels differ, first (y, x) {bad[:4].tolist()}"
+
+
+KINDS = ["true", "identity", "tie_translation", "tie_scale_half", "rot5", "flip_x", "zoom_in", "zoom_out",
+         "far_away", "m8_not_pow2", "projective", "singular"]
+
+
+@pytest.mark.parametrize("w,h", [(640, 480), (1000, 300), (1984, 70), (128, 64), (132, 65), (68, 33)])
+def test_warp_geometries(mdx, wctx, oracle, w, h):
+    g1, g2 = [], []
+    Hs = []
+    for i, kind in enumerate(KINDS):
+        a, b, Ht = mdx.synth_pair(500 + i, w, h, 1)
+        g1.append(a); g2.append(b)
+        Hs.append(_H(kind, w, h, Ht))
+    _run(mdx, wctx, oracle, np.stack(g1), np.stack(g2), Hs, 190)
+
+
+@pytest.mark.parametrize("thresh", [-1, 0, 10, 190, 254, 255, 300])
+def test_warp_thresholds(mdx, wctx, oracle, thresh):
+    w, h = 640, 480
+    a, b, Ht = mdx.synth_pair(77, w, h, 1)
+    a2, b2, _ = mdx.synth_pair(78, w, h, 1)
+    _run(mdx, wctx, oracle, np.stack([a, a2]), np.stack([b, b2]), [Ht, _H("rot5", w, h, Ht)], thresh)
+
+
+def test_warp_4k_true_h(mdx, wctx, oracle):
+    """The roofline workload's geometry (bench.py --only-roofline), one pair."""
+    w, h = 3840, 2160
+    a, b, Ht = mdx.synth_pair(20141105, w, h, 1)
+    _run(mdx, wctx, oracle, a[None], b[None], [Ht], 190)
