@@ -168,6 +168,28 @@ int mdx_band_flow_dev(mdx_ctx* ctx, const uint8_t* d_img1, const uint8_t* d_img2
 int mdx_band_fit_warp_dev(mdx_ctx* ctx, int nrec, const mdx_band_cand* d_cands, int y0, int y1,
                           uint8_t* d_mask_band, double* d_H, int* d_num_vectors);
 
+/*
+ * Trajectory tracking: replaces OpticalFlowCalculator::calculateOpticalFlowTrajectory
+ * (optical_flow_calculator.h:20-21, optical_flow_calculator.cpp:133-257), the node's live caller
+ * (motion_detection_node.cpp:94-110 over 2*num_motions+1 frames, :241).  Synchronous.
+ *   imgs        nimg >= 2 host frames, each w x h, row pitch `stride`, format `fmt`.
+ * The pixel_step grid is tracked through the nimg-1 consecutive pairs; each pass starts from the
+ * points the previous one left (a point moves only when tracked and strictly inside the 10-px
+ * border, :207-216).  Outputs (any may be NULL; npts = mdx_grid_count(w, h, pixel_step)):
+ *   traj        [npts][nimg][2] float  point i's positions: its grid point, then each accepted
+ *               move (entries past traj_len[i] are unspecified)
+ *   traj_len    [npts] int32           the reference's init_traj_list[i].size(); it reports the
+ *               trajectory iff traj_len[i] == nimg (:244-249)
+ *   start_pts   [npts][2] float        the points entering the last pass (where the reference
+ *               stores each Vec4d: optical_flow_vectors.at<Vec4d>((int)y, (int)x))
+ *   vectors     [npts][4] double       the last pass's Vec4d per point (:183-206, :220-230)
+ *   num_vectors                        the reference's return value (last pass only)
+ * Grows the context's pyramid workspace to nimg - 1 slots (one per pair) when needed.
+ */
+int mdx_flow_trajectory(mdx_ctx* ctx, const uint8_t* const* imgs, int nimg, int w, int h, int stride,
+                        int fmt, float* traj, int32_t* traj_len, float* start_pts, double* vectors,
+                        int* num_vectors);
+
 /* Device memory helpers so hosts without a HIP toolchain (ctypes, cgo, JNI) can stage
  * buffers: allocation on the context's device, copies ordered on its stream. */
 void* mdx_dev_alloc(mdx_ctx* ctx, size_t bytes);

@@ -130,6 +130,9 @@ def lib() -> C.CDLL:
     L.mdx_band_flow_dev.restype = C.c_int
     L.mdx_band_fit_warp_dev.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, vp, vp, vp]
     L.mdx_band_fit_warp_dev.restype = C.c_int
+    L.mdx_flow_trajectory.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp,
+                                      C.POINTER(C.c_int)]
+    L.mdx_flow_trajectory.restype = C.c_int
     _lib = L
     return L
 

@@ -41,6 +41,22 @@ class FlowResult:
     code: int               # MDX_OK or MDX_EDEGENERATE
 
 
+@dataclass
+class TrajectoryResult:
+    num_vectors: int        # reference return value (last pass)
+    traj: np.ndarray        # (npts, nimg, 2) float32: grid point, then each accepted move
+    traj_len: np.ndarray    # (npts,) int32: entries of traj in use (complete iff == nimg)
+    start_pts: np.ndarray   # (npts, 2) float32: points entering the last pass
+    vectors: np.ndarray     # (npts, 4) float64: the last pass's Vec4d per point
+
+    @property
+    def trajectories(self) -> list:
+        """The reference's output list (optical_flow_calculator.cpp:244-249): the complete ones,
+        in grid order, each (nimg, 2)."""
+        nimg = self.traj.shape[1]
+        return [self.traj[i] for i in np.nonzero(self.traj_len == nimg)[0]]
+
+
 class Context:
     """One device context (mdx_ctx): workspace sized at creation, one HIP stream."""
 
@@ -110,6 +126,26 @@ class Context:
                                                   _ptr(nextp), _ptr(status), _ptr(vec), _ptr(mask), _ptr(H), _ptr(Hx),
                                                   C.byref(num)))
         return FlowResult(num.value, nextp, status, vec, mask, H.reshape(3, 3), rc)
+
+    # -- trajectory tracking (drop-in for calculateOpticalFlowTrajectory)
+    def flow_trajectory(self, images, fmt: int | None = None) -> "TrajectoryResult":
+        imgs = [np.ascontiguousarray(im, dtype=np.uint8) for im in images]
+        if len(imgs) < 2 or any(im.shape != imgs[0].shape for im in imgs):
+            raise ValueError("need >= 2 frames of one shape")
+        h, w = imgs[0].shape[:2]
+        if fmt is None:
+            fmt = _lib.FMT_GRAY8 if imgs[0].ndim == 2 else _lib.FMT_RGB8
+        nimg = len(imgs)
+        n = grid_count(w, h, self.params.pixel_step)
+        traj = np.zeros((n, nimg, 2), np.float32)
+        tlen = np.zeros(n, np.int32)
+        start = np.zeros((n, 2), np.float32)
+        vec = np.zeros((n, 4), np.float64)
+        arr = (C.c_void_p * nimg)(*[im.ctypes.data for im in imgs])
+        num = C.c_int(0)
+        self._check(lib().mdx_flow_trajectory(self._h, arr, nimg, w, h, imgs[0].strides[0], fmt, _ptr(traj),
+                                              _ptr(tlen), _ptr(start), _ptr(vec), C.byref(num)))
+        return TrajectoryResult(num.value, traj, tlen, start, vec)
 
     # -- device entries (pointers are ints, e.g. torch.Tensor.data_ptr())
     def flow_warp_diff_batch_dev(self, batch: int, d_img1: int, d_img2: int, w: int, h: int, stride: int,

@@ -37,6 +37,7 @@ struct mdx_ctx {
     DevBuf cls, Abuf, ctab;                  // LK v2: class planes, A sums, residue tables
     DevBuf dbg;                              // LK v2 per-level trace (MDX_LK_DEBUG=1)
     DevBuf csum;                             // classify: per-block summaries
+    DevBuf tin, tcur, tnp, tst, ttraj, tlen, tvec, tstart, tnum;   // trajectory tracking
     bool lk_debug = false;
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
@@ -604,6 +605,93 @@ extern "C" int mdx_flow_warp_diff(mdx_ctx* c, const uint8_t* img1, const uint8_t
     HIP_OR_RETURN(c, hipStreamSynchronize(s));
     if (num_vectors) *num_vectors = num;
     if (c->prm.fit_mode == MDX_FIT_FIRST4 && num < 4) return MDX_EDEGENERATE;
+    return MDX_OK;
+}
+
+// calculateOpticalFlowTrajectory (optical_flow_calculator.cpp:133-257).  Pair slot j holds
+// frames (j, j+1): the gray / pyramid / Scharr stages run batched over all slots in one launch
+// each (the reference rebuilds each frame's pyramid twice, :166-170; these are the same images),
+// then the nimg-1 LK passes run in order on the points the previous pass left.
+extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int nimg, int w, int h, int stride,
+                                   int fmt, float* traj, int32_t* traj_len, float* start_pts, double* vectors,
+                                   int* num_vectors)
+{
+    if (!c) return MDX_EINVAL;
+    if (!imgs || nimg < 2) return set_err(c, MDX_EINVAL, "mdx_flow_trajectory: need >= 2 frames");
+    for (int i = 0; i < nimg; i++)
+        if (!imgs[i]) return set_err(c, MDX_EINVAL, "mdx_flow_trajectory: null frame %d", i);
+    if (w <= 0 || h <= 0) return set_err(c, MDX_EINVAL, "bad frame size");
+    if (fmt < MDX_FMT_GRAY8 || fmt > MDX_FMT_BGR8) return set_err(c, MDX_EINVAL, "bad pixel format %d", fmt);
+    const int cn = fmt == MDX_FMT_GRAY8 ? 1 : 3;
+    if (stride < w * cn) return set_err(c, MDX_EINVAL, "stride %d < w*channels %d", stride, w * cn);
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    const mdx_params& P = c->prm;
+    const int npairs = nimg - 1;
+    const Geometry g = make_geometry(w, h, P.max_level);
+    int rc = ensure_workspace(c, g, npairs);
+    if (rc != MDX_OK) return rc;
+    const int npts = mdx_grid_count(w, h, P.pixel_step);
+    const int ny = (h + P.pixel_step - 1) / P.pixel_step;
+    const size_t pts = (size_t)(npts > 0 ? npts : 1);
+    const size_t fbytes = (size_t)stride * h;
+    if ((rc = ensure(c, c->tin, fbytes * nimg)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->tcur, pts * 8)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->tnp, pts * 8)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->tst, pts)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->ttraj, pts * nimg * 8)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->tlen, pts * 4)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->tvec, pts * 32)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->tstart, pts * 8)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->tnum, 4)) != MDX_OK) return rc;
+
+    hipStream_t s = c->stream;
+    uint8_t* din = c->tin.as<uint8_t>();
+    for (int i = 0; i < nimg; i++)
+        HIP_OR_RETURN(c, hipMemcpyAsync(din + fbytes * i, imgs[i], fbytes, hipMemcpyHostToDevice, s));
+    uint8_t* pyr1 = c->pyr1.as<uint8_t>();
+    uint8_t* pyr2 = c->pyr2.as<uint8_t>();
+    uint32_t* der = c->der.as<uint32_t>();
+    HIP_OR_RETURN(c, launch_gray_pad(s, npairs, din, din + fbytes, w, h, stride, (long long)fbytes, fmt, pyr1, pyr2, g));
+    for (int l = 1; l < g.nlev; l++) HIP_OR_RETURN(c, launch_pyrdown(s, npairs, pyr1, pyr2, g, l));
+    for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, npairs, pyr1, der, g, l));
+    float* cur = c->tcur.as<float>();
+    float* tr = c->ttraj.as<float>();
+    int* tl = c->tlen.as<int>();
+    int* dnum = c->tnum.as<int>();
+    HIP_OR_RETURN(c, launch_traj_init(s, npts, ny, P.pixel_step, nimg, cur, tr, tl, dnum));
+    for (int j = 0; j < npairs && npts > 0; j++) {
+        LkArgs a{};
+        a.pyr1 = pyr1 + (size_t)g.img_bytes * j;
+        a.pyr2 = pyr2 + (size_t)g.img_bytes * j;
+        a.der = der + (size_t)g.der_words * j;
+        a.g = g;
+        a.maxl = g.nlev - 1;
+        a.npts = npts;
+        a.ny = ny;
+        a.nyg = ny;
+        a.pixel_step = P.pixel_step;
+        a.max_iters = std::min(std::max(P.max_iters, 0), 100);
+        a.min_eig = P.min_eig;
+        const double e = std::min(std::max(P.eps, 0.), 10.);
+        a.eps2 = e * e;
+        a.next_pts = c->tnp.as<float>();
+        a.status = c->tst.as<uint8_t>();
+        a.prev_pts = cur;
+        HIP_OR_RETURN(c, launch_lk(s, 1, a));
+        HIP_OR_RETURN(c, launch_traj_update(s, npts, c->tnp.as<float>(), c->tst.as<uint8_t>(), cur, tr, tl, nimg, w, h,
+                                            j == npairs - 1, P.min_vector_size, c->tvec.as<double>(),
+                                            c->tstart.as<float>(), dnum));
+    }
+    int num = 0;
+    if (npts > 0) {
+        if (traj) HIP_OR_RETURN(c, hipMemcpyAsync(traj, tr, (size_t)npts * nimg * 8, hipMemcpyDeviceToHost, s));
+        if (traj_len) HIP_OR_RETURN(c, hipMemcpyAsync(traj_len, tl, (size_t)npts * 4, hipMemcpyDeviceToHost, s));
+        if (start_pts) HIP_OR_RETURN(c, hipMemcpyAsync(start_pts, c->tstart.p, (size_t)npts * 8, hipMemcpyDeviceToHost, s));
+        if (vectors) HIP_OR_RETURN(c, hipMemcpyAsync(vectors, c->tvec.p, (size_t)npts * 32, hipMemcpyDeviceToHost, s));
+    }
+    HIP_OR_RETURN(c, hipMemcpyAsync(&num, dnum, 4, hipMemcpyDeviceToHost, s));
+    HIP_OR_RETURN(c, hipStreamSynchronize(s));
+    if (num_vectors) *num_vectors = num;
     return MDX_OK;
 }
 

@@ -96,6 +96,7 @@ struct LkArgs {
     const int16_t* rlist;    // [level][axis][128] class index -> residue
     const int16_t* ord;      // per level: nxp padded grid columns (-1 = empty), then ny grid rows,
                              // both grouped by residue class (ClassLevel::ord_off)
+    const float* prev_pts;   // k_lk only: [batch][npts][2] start points (trajectories); null = the grid
     float4* dbg;             // optional [batch][nlev][npts] (npx, npy, iters, status) at level end
     int dbg_pt;              // point whose per-iteration values are appended after dbg (pair 0)
 };
@@ -107,6 +108,12 @@ hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const u
 hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level);
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level);
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
+// Trajectory tracking (calculateOpticalFlowTrajectory): grid init and the per-pass point update.
+hipError_t launch_traj_init(hipStream_t s, int npts, int ny, int pixel_step, int nimg, float* cur, float* traj,
+                            int* tlen, int* num);
+hipError_t launch_traj_update(hipStream_t s, int npts, const float* next_pts, const uint8_t* status, float* cur,
+                              float* traj, int* tlen, int nimg, int w, int h, int last, double min_vector_size,
+                              double* vectors, float* start_pts, int* num);
 // Ab: [nlev][batch][npts] per-point (A11, A12, A22, 1/D); qctr: [batch][kMaxLevels][8] queue
 // heads.  aux (may be null): second stream for the flow-independent class / A kernels; ev: kMaxLevels
 // + 1 events (no timing) used to order the two streams.

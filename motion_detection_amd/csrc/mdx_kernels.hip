@@ -247,7 +247,12 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a)
     }
 
     const int gx = valid ? pt / a.ny : 0, gy = valid ? pt % a.ny : 0;
-    const float px0 = (float)(gx * a.pixel_step), py0 = (float)(gy * a.pixel_step);
+    float px0 = (float)(gx * a.pixel_step), py0 = (float)(gy * a.pixel_step);
+    if (a.prev_pts && valid) {   // trajectory passes: arbitrary start points (flags 0: nextPt = prevPt)
+        const float* pp = a.prev_pts + ((long long)pair * a.npts + pt) * 2;
+        px0 = pp[0];
+        py0 = pp[1];
+    }
     float npx = 0.f, npy = 0.f;   // nextPts[ptidx]
     int status = 1;
 
@@ -886,6 +891,81 @@ hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t
     const int nchunk = (kXOff + L.w + kPad - 1) / 4;                 // last 4-word chunk
     const dim3 grid((nchunk - 4 + 1 + 63) / 64, L.h + 2 * kPad, batch);
     hipLaunchKernelGGL(k_scharr, grid, dim3(64), 0, s, pyr1, der, g.img_bytes, g.der_words, L, nchunk);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ trajectory tracking
+// OpticalFlowCalculator::calculateOpticalFlowTrajectory (optical_flow_calculator.cpp:133-257).
+// init: points = the grid (:148-158, x-major), every trajectory = its grid point.
+__global__ void k_traj_init(int npts, int ny, int pixel_step, int nimg, float* __restrict__ cur,
+                            float* __restrict__ traj, int* __restrict__ tlen, int* __restrict__ num)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *num = 0;
+    if (i >= npts) return;
+    const float x = (float)((i / ny) * pixel_step), y = (float)((i % ny) * pixel_step);
+    cur[2 * i] = x;
+    cur[2 * i + 1] = y;
+    traj[(long long)i * nimg * 2] = x;
+    traj[(long long)i * nimg * 2 + 1] = y;
+    tlen[i] = 1;
+}
+
+// One pass j -> j+1 (:178-242): a tracked point moves (and its trajectory grows) only when it lands
+// strictly inside the 10-px border; lost or border points stay.  On the last pass the Vec4d of
+// :183-206 / :220-230 per point and num_vectors (order-free integer count).
+__global__ void k_traj_update(int npts, const float* __restrict__ next_pts, const uint8_t* __restrict__ status,
+                              float* __restrict__ cur, float* __restrict__ traj, int* __restrict__ tlen, int nimg, int w,
+                              int h, int last, double min_vector_size, double* __restrict__ vectors,
+                              float* __restrict__ start_pts, int* __restrict__ num)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npts) return;
+    const float sx = cur[2 * i], sy = cur[2 * i + 1];
+    double* v = (last && vectors) ? vectors + 4LL * i : nullptr;
+    if (last && start_pts) {
+        start_pts[2 * i] = sx;
+        start_pts[2 * i + 1] = sy;
+    }
+    if (status[i]) {
+        const float ex = next_pts[2 * i], ey = next_pts[2 * i + 1];
+        if (last) {
+            const float xd = ex - sx, yd = ey - sy;
+            if (fabs((double)fabsf(xd)) > min_vector_size || fabs((double)fabsf(yd)) > min_vector_size) {
+                if (v) { v[0] = sx; v[1] = sy; v[2] = xd; v[3] = yd; }
+                atomicAdd(num, 1);
+            } else if (v) {
+                v[0] = sx; v[1] = sy; v[2] = 0.0; v[3] = 0.0;
+            }
+        }
+        if (ex > 10.0f && ey > 10.0f && ex < (float)(w - 10) && ey < (float)(h - 10)) {
+            cur[2 * i] = ex;
+            cur[2 * i + 1] = ey;
+            const int l = tlen[i];
+            traj[((long long)i * nimg + l) * 2] = ex;
+            traj[((long long)i * nimg + l) * 2 + 1] = ey;
+            tlen[i] = l + 1;
+        }
+    } else if (v) {
+        v[0] = -1.0; v[1] = -1.0; v[2] = 0.0; v[3] = 0.0;
+    }
+}
+
+hipError_t launch_traj_init(hipStream_t s, int npts, int ny, int pixel_step, int nimg, float* cur, float* traj,
+                            int* tlen, int* num)
+{
+    hipLaunchKernelGGL(k_traj_init, dim3((npts + 255) / 256 > 0 ? (npts + 255) / 256 : 1), dim3(256), 0, s, npts, ny,
+                       pixel_step, nimg, cur, traj, tlen, num);
+    return hipGetLastError();
+}
+
+hipError_t launch_traj_update(hipStream_t s, int npts, const float* next_pts, const uint8_t* status, float* cur,
+                              float* traj, int* tlen, int nimg, int w, int h, int last, double min_vector_size,
+                              double* vectors, float* start_pts, int* num)
+{
+    if (npts <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_traj_update, dim3((npts + 255) / 256), dim3(256), 0, s, npts, next_pts, status, cur, traj,
+                       tlen, nimg, w, h, last, min_vector_size, vectors, start_pts, num);
     return hipGetLastError();
 }
 

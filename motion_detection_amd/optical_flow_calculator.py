@@ -18,6 +18,19 @@ argument meaning and return value; the output Mats become numpy arrays filled in
   (:118-128).  With 1..3 vectors the reference reads past src_points (UB); here comp is
   zero-filled instead.
 
+calculateOpticalFlowTrajectory (:133-257), the node's live caller (node.cpp:94-110), has the
+same form:
+
+    num_vectors = ofc.calculateOpticalFlowTrajectory(images, optical_flow_vectors, trajectories,
+                                                     pixel_step, comp, min_vector_size)
+
+* images: list of >= 2 frames (rgb8 or mono8).
+* optical_flow_vectors: (h, w, 4) float64; the last pass's Vec4d of every point is stored at
+  [(int)y, (int)x] of the point entering that pass, in point order (later points overwrite
+  earlier ones at the same pixel, as the reference's stores do).
+* trajectories: a list, extended with the complete trajectories ((nimg, 2) float32 arrays).
+* comp is not touched (the reference never writes it here).
+
 All arithmetic runs on the MI355X through libmdx.so; there is no CPU fallback.
 """
 from __future__ import annotations
@@ -60,6 +73,23 @@ class OpticalFlowCalculator:
             optical_flow_vectors[pts[:, 1], pts[:, 0], :] = res.vectors
         if comp is not None and res.num_vectors > 0:
             comp[...] = res.mask
+        return res.num_vectors
+
+    def calculateOpticalFlowTrajectory(self, images, optical_flow_vectors: np.ndarray | None, trajectories: list,
+                                       pixel_step: int, comp: np.ndarray | None, min_vector_size: float) -> int:
+        imgs = [np.asarray(im) for im in images]
+        h, w = imgs[0].shape[:2]
+        fmt = _lib.FMT_GRAY8 if imgs[0].ndim == 2 else _lib.FMT_RGB8
+        ctx = self._context(w, h, pixel_step, min_vector_size)
+        res = ctx.flow_trajectory(imgs, fmt=fmt)
+        if optical_flow_vectors is not None:
+            if optical_flow_vectors.shape[:2] != (h, w) or optical_flow_vectors.shape[-1] != 4:
+                raise ValueError("optical_flow_vectors must be (h, w, 4)")
+            ix = res.start_pts.astype(np.int64)   # (int) truncation of the float position
+            ok = (ix[:, 0] >= 0) & (ix[:, 0] < w) & (ix[:, 1] >= 0) & (ix[:, 1] < h)
+            for i in np.nonzero(ok)[0]:           # point order: last store wins
+                optical_flow_vectors[ix[i, 1], ix[i, 0], :] = res.vectors[i]
+        trajectories.extend(res.trajectories)
         return res.num_vectors
 
     def compute(self, image1: np.ndarray, image2: np.ndarray, pixel_step: int = 10, min_vector_size: float = 1.0,

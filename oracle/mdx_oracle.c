@@ -814,3 +814,73 @@ int ora_calculate_optical_flow(const uint8_t* img1, const uint8_t* img2, int w, 
     free(g1); free(g2); free(pts1); free(pts2); free(st);
     return num;
 }
+
+/* ------------------------------------------------- trajectory tracking - */
+/* OpticalFlowCalculator::calculateOpticalFlowTrajectory (reference
+ * common/src/optical_flow_calculator.cpp:133-257), restated.  Per consecutive pair j -> j+1
+ * (:161): gray both frames (:166-167), pyramid of frame j with derivatives (:170), LK of the
+ * current points (:172, flags 0: each pass starts from the point itself).  Per point (:178-236):
+ *   status set: on the last pair (:183-206) the Vec4d (x, y, dx, dy) if |dx| or |dy| exceeds
+ *     min_vector_size (num_vectors++), else (x, y, 0, 0), with (x, y) the point before the pass;
+ *     then if 10 < x' < cols-10 and 10 < y' < rows-10 (:207-208) the point moves to x' and its
+ *     trajectory grows by x' (:210-211), else it stays (:215);
+ *   status clear: on the last pair (-1, -1, 0, 0) (:220-230); the point stays (:234).
+ * traj[i] holds the init_traj_list entries (:143-158, :211), traj_len[i] their count; a
+ * trajectory is reported by the reference iff traj_len == nimg (:244-249).  start_pts receives
+ * the points entering the last pass (the Vec4d's buffer position).  Returns num_vectors. */
+int ora_flow_trajectory(const uint8_t* const* imgs, int nimg, int w, int h, int stride, int fmt,
+                        const ora_params* prm, int nthreads, float* traj, int* traj_len,
+                        float* start_pts, double* vectors)
+{
+    const int npts = ora_grid_count(w, h, prm->pixel_step);
+    const size_t np1 = (size_t)(npts > 0 ? npts : 1);
+    float* cur = (float*)malloc(sizeof(float) * 2 * np1);
+    float* nxt = (float*)malloc(sizeof(float) * 2 * np1);
+    uint8_t* st = (uint8_t*)malloc(np1);
+    int* len = (int*)malloc(sizeof(int) * np1);
+    uint8_t* g1 = (uint8_t*)malloc((size_t)w * h);
+    uint8_t* g2 = (uint8_t*)malloc((size_t)w * h);
+    ora_grid_points(w, h, prm->pixel_step, cur);
+    for (int i = 0; i < npts; i++) {
+        len[i] = 1;
+        if (traj) { traj[(size_t)i * nimg * 2] = cur[2 * i]; traj[(size_t)i * nimg * 2 + 1] = cur[2 * i + 1]; }
+    }
+    int num = 0;
+    for (int j = 0; j + 1 < nimg; j++) {
+        const int last = (j == nimg - 2);
+        ora_to_gray(imgs[j], w, h, stride, fmt, g1);
+        ora_to_gray(imgs[j + 1], w, h, stride, fmt, g2);
+        ora_pyramid P1, P2;
+        int ml = ora_build_pyramid(g1, w, h, prm->win, prm->max_level, 1, &P1);
+        ml = ora_build_pyramid(g2, w, h, prm->win, ml, 0, &P2);
+        ora_lk(&P1, &P2, ml, cur, nxt, st, npts, prm, nthreads);
+        ora_free_pyramid(&P1);
+        ora_free_pyramid(&P2);
+        for (int i = 0; i < npts; i++) {
+            const float sx = cur[2 * i], sy = cur[2 * i + 1];
+            double* v = (last && vectors) ? vectors + 4 * (size_t)i : NULL;
+            if (last && start_pts) { start_pts[2 * i] = sx; start_pts[2 * i + 1] = sy; }
+            if (st[i]) {
+                const float ex = nxt[2 * i], ey = nxt[2 * i + 1];
+                if (last) {
+                    const float xd = ex - sx, yd = ey - sy;
+                    if (fabs((double)fabsf(xd)) > prm->min_vector_size || fabs((double)fabsf(yd)) > prm->min_vector_size) {
+                        if (v) { v[0] = sx; v[1] = sy; v[2] = xd; v[3] = yd; }
+                        num++;
+                    } else if (v) { v[0] = sx; v[1] = sy; v[2] = 0.0; v[3] = 0.0; }
+                }
+                if (ex > 10.0f && ey > 10.0f && ex < (float)(w - 10) && ey < (float)(h - 10)) {
+                    cur[2 * i] = ex; cur[2 * i + 1] = ey;
+                    if (traj) {
+                        traj[((size_t)i * nimg + len[i]) * 2] = ex;
+                        traj[((size_t)i * nimg + len[i]) * 2 + 1] = ey;
+                    }
+                    len[i]++;
+                }
+            } else if (v) { v[0] = -1.0; v[1] = -1.0; v[2] = 0.0; v[3] = 0.0; }
+        }
+    }
+    if (traj_len) memcpy(traj_len, len, sizeof(int) * (size_t)npts);
+    free(cur); free(nxt); free(st); free(len); free(g1); free(g2);
+    return num;
+}

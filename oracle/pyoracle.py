@@ -67,6 +67,9 @@ def lib():
                                                  C.POINTER(OraParams), C.c_int, f32p, u8p, f64p, u8p,
                                                  f64p, f64p, C.POINTER(C.c_int)]
         L.ora_calculate_optical_flow.restype = C.c_int
+        L.ora_flow_trajectory.argtypes = [C.POINTER(u8p), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                          C.POINTER(OraParams), C.c_int, f32p, C.POINTER(C.c_int), f32p, f64p]
+        L.ora_flow_trajectory.restype = C.c_int
         _lib = L
     return _lib
 
@@ -175,3 +178,48 @@ def calculate_optical_flow(img1: np.ndarray, img2: np.ndarray, fmt: int | None =
         _p(mask, C.c_uint8) if mask is not None else None, _p(H, C.c_double), _p(Hinv, C.c_double), C.byref(fs))
     return dict(num_vectors=num, next_pts=nextp, status=status, vectors=vec, mask=mask,
                 H=H.reshape(3, 3), Hinv=Hinv.reshape(3, 3), fit_status=fs.value)
+
+
+def flow_trajectory(images, fmt: int | None = None, nthreads: int = 1, **kw):
+    """calculateOpticalFlowTrajectory (optical_flow_calculator.cpp:133-257) over a list of frames.
+    Returns dict(num_vectors, traj (npts, nimg, 2), traj_len (npts,), start_pts (npts, 2),
+    vectors (npts, 4), trajectories = [traj[i] for complete i] as the reference reports them)."""
+    imgs = [np.ascontiguousarray(im) for im in images]
+    nimg = len(imgs)
+    h, w = imgs[0].shape[:2]
+    if fmt is None:
+        fmt = FMT_GRAY8 if imgs[0].ndim == 2 else FMT_RGB8
+    prm = params(**kw)
+    n = grid_count(w, h, prm.pixel_step)
+    traj = np.zeros((n, nimg, 2), np.float32)
+    tlen = np.zeros(n, np.int32)
+    start = np.zeros((n, 2), np.float32)
+    vec = np.zeros((n, 4), np.float64)
+    arr = (C.POINTER(C.c_uint8) * nimg)(*[_p(im, C.c_uint8) for im in imgs])
+    num = lib().ora_flow_trajectory(arr, nimg, w, h, imgs[0].strides[0], fmt, C.byref(prm), nthreads,
+                                    _p(traj, C.c_float), tlen.ctypes.data_as(C.POINTER(C.c_int)),
+                                    _p(start, C.c_float), _p(vec, C.c_double))
+    full = [traj[i] for i in range(n) if tlen[i] == nimg]
+    return dict(num_vectors=num, traj=traj, traj_len=tlen, start_pts=start, vectors=vec, trajectories=full)
+
+
+def lk(gray1: np.ndarray, gray2: np.ndarray, prev_pts: np.ndarray, nthreads: int = 1, **kw):
+    """calcOpticalFlowPyrLK(buildOpticalFlowPyramid(gray1), gray2, prev_pts, ...) with the
+    reference's arguments (optical_flow_calculator.cpp:67-71 / :170-172).  Returns (next_pts, status)."""
+    gray1 = np.ascontiguousarray(gray1)
+    gray2 = np.ascontiguousarray(gray2)
+    h, w = gray1.shape
+    prm = params(**kw)
+    pts = np.ascontiguousarray(prev_pts, dtype=np.float32).reshape(-1, 2)
+    n = len(pts)
+    nxt = np.zeros((max(n, 1), 2), np.float32)
+    st = np.zeros(max(n, 1), np.uint8)
+    P1, P2 = OraPyramid(), OraPyramid()
+    L = lib()
+    ml = L.ora_build_pyramid(_p(gray1, C.c_uint8), w, h, prm.win, prm.max_level, 1, C.byref(P1))
+    ml = L.ora_build_pyramid(_p(gray2, C.c_uint8), w, h, prm.win, ml, 0, C.byref(P2))
+    L.ora_lk(C.byref(P1), C.byref(P2), ml, _p(pts, C.c_float), _p(nxt, C.c_float), _p(st, C.c_uint8), n,
+             C.byref(prm), nthreads)
+    L.ora_free_pyramid(C.byref(P1))
+    L.ora_free_pyramid(C.byref(P2))
+    return nxt[:n], st[:n]
