@@ -20,7 +20,7 @@ for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         if "k_warp_diff" not in r["Kernel_Name"]:
             continue
-        # the roofline launches are the large grids (w*h*b/32 threads for 64x128 tiles of 256)
+        # the roofline launches are the large grids (w*h*b/32 threads: 128x64 tiles of 256 threads)
         if int(r["Grid_Size"]) < (w * h * b) // 64:
             continue
         vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
