@@ -190,6 +190,30 @@ int mdx_flow_trajectory(mdx_ctx* ctx, const uint8_t* const* imgs, int nimg, int 
                         int fmt, float* traj, int32_t* traj_len, float* start_pts, double* vectors,
                         int* num_vectors);
 
+/*
+ * Trajectory subspace RANSAC: replaces OutlierDetector::fitSubspace
+ * (common/include/motion_detection/outlier_detector.h:21, outlier_detector.cpp:236-331), called
+ * by the node on the complete trajectories (motion_detection_node.cpp:348).
+ *   traj        [ntraj][traj_len][2] float host trajectories (mdx_flow_trajectory's complete ones)
+ *   rng         the caller's generator: the reference draws 50 x 4*num_motions samples per call
+ *               from one srand(time(NULL)) stream (outlier_detector.cpp:17, :226); seed it with
+ *               mdx_srand (glibc rand() restated: the same stream for the same seed)
+ * Outputs (any may be NULL):
+ *   columns     [4*num_motions] the winning sample's trajectory indices (the return value of
+ *               fitSubspace is those trajectories); -1 when no hypothesis had an inlier
+ *   is_outlier  [ntraj] 1 where the winner's residual exceeds sigma^2 * chi2_99[n-d]
+ *   residuals   [ntraj] double, the winner's residuals
+ *   outlier_points [n_outliers][2] float: each outlier's second-to-last point (:322), in order
+ * Arithmetic: the reference's float meanSubtract; double Householder QR of each sample and
+ * double residuals (the reference: Eigen float JacobiSVD; see DESIGN.md §7c for parity).
+ */
+typedef struct mdx_rand_state { uint32_t x[34]; int32_t pos; } mdx_rand_state;
+void mdx_srand(mdx_rand_state* st, uint32_t seed);
+int  mdx_rand(mdx_rand_state* st);
+int  mdx_fit_subspace(mdx_ctx* ctx, const float* traj, int ntraj, int traj_len, int num_motions, double sigma,
+                      mdx_rand_state* rng, int* columns, uint8_t* is_outlier, double* residuals,
+                      float* outlier_points, int* n_outliers);
+
 /* Device memory helpers so hosts without a HIP toolchain (ctypes, cgo, JNI) can stage
  * buffers: allocation on the context's device, copies ordered on its stream. */
 void* mdx_dev_alloc(mdx_ctx* ctx, size_t bytes);

@@ -34,6 +34,7 @@ EXPORTED = [
     "mdx_flow_warp_diff", "mdx_flow_warp_diff_batch_dev", "mdx_warp_diff_dev", "mdx_dev_alloc",
     "mdx_dev_free", "mdx_memcpy_h2d", "mdx_memcpy_d2h", "mdx_enable_timing", "mdx_timing_calls", "mdx_stage_ms",
     "mdx_synth_pair", "mdx_debug_copy", "mdx_band_flow_dev", "mdx_band_fit_warp_dev", "mdx_flow_trajectory",
+    "mdx_srand", "mdx_rand", "mdx_fit_subspace",
 ]
 
 
@@ -41,6 +42,11 @@ class MdxBandCand(C.Structure):
     """mdx_band_cand (include/mdx.h): one row band's accepted count and first four accepted points."""
     _fields_ = [("count", C.c_int32), ("n", C.c_int32), ("idx", C.c_int32 * 4), ("src", C.c_float * 8),
                 ("dst", C.c_float * 8), ("pad_", C.c_int32 * 2)]
+
+
+class MdxRandState(C.Structure):
+    """mdx_rand_state (include/mdx.h): glibc rand() generator state."""
+    _fields_ = [("x", C.c_uint32 * 34), ("pos", C.c_int32)]
 
 
 BAND_CAND_BYTES = 96
@@ -133,6 +139,13 @@ def lib() -> C.CDLL:
     L.mdx_flow_trajectory.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp,
                                       C.POINTER(C.c_int)]
     L.mdx_flow_trajectory.restype = C.c_int
+    L.mdx_srand.argtypes = [C.POINTER(MdxRandState), C.c_uint32]
+    L.mdx_srand.restype = None
+    L.mdx_rand.argtypes = [C.POINTER(MdxRandState)]
+    L.mdx_rand.restype = C.c_int
+    L.mdx_fit_subspace.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_double, C.POINTER(MdxRandState), vp, vp, vp,
+                                   vp, C.POINTER(C.c_int)]
+    L.mdx_fit_subspace.restype = C.c_int
     _lib = L
     return L
 

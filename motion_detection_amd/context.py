@@ -57,6 +57,14 @@ class TrajectoryResult:
         return [self.traj[i] for i in np.nonzero(self.traj_len == nimg)[0]]
 
 
+@dataclass
+class SubspaceResult:
+    columns: np.ndarray         # (4*num_motions,) int32: the winning sample (-1: no hypothesis had an inlier)
+    is_outlier: np.ndarray      # (ntraj,) uint8
+    residuals: np.ndarray       # (ntraj,) float64, the winner's
+    outlier_points: np.ndarray  # (n_outliers, 2) float32: each outlier's second-to-last point
+
+
 class Context:
     """One device context (mdx_ctx): workspace sized at creation, one HIP stream."""
 
@@ -146,6 +154,22 @@ class Context:
         self._check(lib().mdx_flow_trajectory(self._h, arr, nimg, w, h, imgs[0].strides[0], fmt, _ptr(traj),
                                               _ptr(tlen), _ptr(start), _ptr(vec), C.byref(num)))
         return TrajectoryResult(num.value, traj, tlen, start, vec)
+
+    # -- trajectory subspace RANSAC (drop-in for OutlierDetector::fitSubspace)
+    def fit_subspace(self, traj: np.ndarray, num_motions: int, sigma: float, rng: "_lib.MdxRandState") -> "SubspaceResult":
+        traj = np.ascontiguousarray(traj, dtype=np.float32)
+        if traj.ndim != 3 or traj.shape[2] != 2:
+            raise ValueError("traj must be (ntraj, traj_len, 2)")
+        N, T = traj.shape[:2]
+        d = 4 * num_motions
+        cols = np.full(d, -1, np.int32)
+        out = np.zeros(N, np.uint8)
+        res = np.zeros(N, np.float64)
+        pts = np.zeros((N, 2), np.float32)
+        nout = C.c_int(0)
+        self._check(lib().mdx_fit_subspace(self._h, _ptr(traj), N, T, int(num_motions), float(sigma), C.byref(rng),
+                                           _ptr(cols), _ptr(out), _ptr(res), _ptr(pts), C.byref(nout)))
+        return SubspaceResult(cols, out, res, pts[:nout.value].copy())
 
     # -- device entries (pointers are ints, e.g. torch.Tensor.data_ptr())
     def flow_warp_diff_batch_dev(self, batch: int, d_img1: int, d_img2: int, w: int, h: int, stride: int,

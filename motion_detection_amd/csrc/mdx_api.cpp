@@ -38,6 +38,7 @@ struct mdx_ctx {
     DevBuf dbg;                              // LK v2 per-level trace (MDX_LK_DEBUG=1)
     DevBuf csum;                             // classify: per-block summaries
     DevBuf tin, tcur, tnp, tst, ttraj, tlen, tvec, tstart, tnum;   // trajectory tracking
+    DevBuf straj, sdata, sq, scnt, scols, sres, sout, sbest;      // subspace RANSAC
     bool lk_debug = false;
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
@@ -692,6 +693,94 @@ extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int n
     HIP_OR_RETURN(c, hipMemcpyAsync(&num, dnum, 4, hipMemcpyDeviceToHost, s));
     HIP_OR_RETURN(c, hipStreamSynchronize(s));
     if (num_vectors) *num_vectors = num;
+    return MDX_OK;
+}
+
+// glibc rand() (random_r TYPE_3), the generator of fitSubspace's samples
+// (outlier_detector.cpp:17 srand(time(NULL)), :226 rand() % data.cols()).
+extern "C" void mdx_srand(mdx_rand_state* st, uint32_t seed)
+{
+    int32_t r[34];
+    r[0] = (int32_t)(seed ? seed : 1u);
+    for (int i = 1; i < 31; i++) {
+        const int64_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+        int64_t word = 16807 * lo - 2836 * hi;
+        if (word < 0) word += 2147483647;
+        r[i] = (int32_t)word;
+    }
+    for (int i = 31; i < 34; i++) r[i] = r[i - 31];
+    for (int i = 0; i < 34; i++) st->x[i] = (uint32_t)r[i];
+    st->pos = 34;
+    for (int k = 0; k < 310; k++) (void)mdx_rand(st);
+}
+
+extern "C" int mdx_rand(mdx_rand_state* st)
+{
+    const int i = st->pos;                       // ring of 34: x[i] = x[i-31] + x[i-3]
+    const uint32_t v = st->x[(i - 31) % 34] + st->x[(i - 3) % 34];
+    st->x[i % 34] = v;
+    st->pos = (i + 1) % 34 + 34;
+    return (int)(v >> 1);
+}
+
+// fitSubspace (outlier_detector.cpp:236-331): samples drawn on the host from the caller's
+// generator state (the reference's OutlierDetector keeps one stream across calls), the rest on
+// the device (mdx_subspace.hip).
+extern "C" int mdx_fit_subspace(mdx_ctx* c, const float* traj, int ntraj, int traj_len, int num_motions, double sigma,
+                                mdx_rand_state* rng, int* columns, uint8_t* is_outlier, double* residuals,
+                                float* outlier_points, int* n_outliers)
+{
+    if (!c) return MDX_EINVAL;
+    const int n = 2 * traj_len, d = 4 * num_motions;
+    if (!traj || !rng || ntraj <= 0 || traj_len < 1 || num_motions < 1)
+        return set_err(c, MDX_EINVAL, "mdx_fit_subspace: bad argument (the reference needs >= 1 trajectory: rand() %% 0)");
+    if (d > n) return set_err(c, MDX_EINVAL, "mdx_fit_subspace: 4*num_motions > 2*traj_len (reference reads U past its columns)");
+    if (n > 32) return set_err(c, MDX_EINVAL, "mdx_fit_subspace: trajectories longer than 16 points");
+    if (n - d == 10) return set_err(c, MDX_EINVAL, "mdx_fit_subspace: n - d == 10 (reference chi_square_table.at(10) throws)");
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    constexpr int kHyp = 50;                      // num_iterations (:250)
+    std::vector<int> cols((size_t)kHyp * d);
+    for (auto& v : cols) v = mdx_rand(rng) % ntraj;   // fillSubset, hypothesis by hypothesis (:223-230)
+    const size_t N = (size_t)ntraj;
+    int rc;
+    if ((rc = ensure(c, c->straj, N * n * 4)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->sdata, N * n * 4)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->sq, (size_t)kHyp * n * std::max(n - d, 1) * 8)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->scnt, kHyp * 4)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->scols, cols.size() * 4)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->sres, N * 8)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->sout, N)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->sbest, 4)) != MDX_OK) return rc;
+    hipStream_t s = c->stream;
+    HIP_OR_RETURN(c, hipMemcpyAsync(c->straj.p, traj, N * n * 4, hipMemcpyHostToDevice, s));
+    HIP_OR_RETURN(c, hipMemcpyAsync(c->scols.p, cols.data(), cols.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_OR_RETURN(c, launch_subspace(s, c->straj.as<float>(), ntraj, traj_len, d, c->scols.as<int>(), kHyp, sigma,
+                                     c->sdata.as<float>(), c->sq.as<double>(), c->scnt.as<int>(), c->sres.as<double>(),
+                                     c->sout.as<uint8_t>(), c->sbest.as<int>()));
+    std::vector<uint8_t> out(N);
+    int best = -1;
+    HIP_OR_RETURN(c, hipMemcpyAsync(out.data(), c->sout.p, N, hipMemcpyDeviceToHost, s));
+    if (residuals) HIP_OR_RETURN(c, hipMemcpyAsync(residuals, c->sres.p, N * 8, hipMemcpyDeviceToHost, s));
+    HIP_OR_RETURN(c, hipMemcpyAsync(&best, c->sbest.p, 4, hipMemcpyDeviceToHost, s));
+    HIP_OR_RETURN(c, hipStreamSynchronize(s));
+    int nout = 0;
+    for (size_t i = 0; i < N; i++) {
+        if (!out[i]) continue;
+        if (outlier_points) {     // the trajectory's second-to-last point (:322)
+            const int j = traj_len >= 2 ? traj_len - 2 : 0;
+            outlier_points[2 * nout] = traj[(i * traj_len + j) * 2];
+            outlier_points[2 * nout + 1] = traj[(i * traj_len + j) * 2 + 1];
+        }
+        nout++;
+    }
+    if (is_outlier) std::memcpy(is_outlier, out.data(), N);
+    if (columns) {
+        if (best >= 0)
+            std::memcpy(columns, cols.data() + (size_t)best * d, (size_t)d * 4);
+        else
+            for (int k = 0; k < d; k++) columns[k] = -1;
+    }
+    if (n_outliers) *n_outliers = nout;
     return MDX_OK;
 }
 

@@ -1,0 +1,182 @@
+// mdx_subspace.hip -- trajectory subspace RANSAC:
+// OutlierDetector::fitSubspace (reference common/src/outlier_detector.cpp:236-331).
+//
+//   data      n x N floats, column i = trajectory i's (x, y) points, mean-subtracted with the
+//             reference's quirks (meanSubtract :200-221: the means of rows 0 / 1 only, float sums
+//             in column order, y flipped)                                   -> k_subspace_prep
+//   50 x      d = 4*num_motions columns drawn by rand() % N (host-side glibc rand restatement);
+//             Pnd = I - U_d U_d' from the sample's SVD = Q2 Q2' with Q2 the last n - d columns of
+//             the sample's Householder Q; residual_i = |x_i' Pnd x_i| = ||Q2' x_i||^2; inliers:
+//             residual < (n - d) sigma^2                                     -> k_subspace_hyp
+//   winner    the first hypothesis with the most inliers (strict >, :300); outliers: its residual
+//             > sigma^2 chi2_99[n - d] (:312-323)                            -> k_subspace_final
+//
+// One workgroup per hypothesis: lane 0 factors the tiny n x d sample (n <= 32) in double, the
+// workgroup then streams all N columns (2n MACs each) and reduces its inlier count.  The double
+// arithmetic follows the oracle's restatement (oracle/mdx_oracle.c subspace_basis /
+// subspace_residual) operation for operation, un-fused, so both round identically.
+#include "mdx_internal.h"
+
+namespace mdx {
+
+constexpr int kMaxSub = 32;   // n = 2 * trajectory length (reference: 10 / 14 / 18 for 2..4 motions)
+
+// meanSubtract.  One workgroup: the row-0 / row-1 sums are sequential float sums (Eigen's
+// row().sum() on a column-major matrix visits the columns in order), staged through LDS in
+// chunks so lane 0's dependent adds read LDS, not HBM.
+__global__ __launch_bounds__(256) void k_subspace_prep(const float* __restrict__ traj, int N, int T,
+                                                        float* __restrict__ data)
+{
+    constexpr int kChunk = 4096;
+    __shared__ float sx[kChunk], sy[kChunk];
+    __shared__ float s_mean[2];
+    const int tid = threadIdx.x;
+    float xs = 0.f, ys = 0.f;
+    for (int base = 0; base < N; base += kChunk) {
+        const int m = min(kChunk, N - base);
+        for (int i = tid; i < m; i += 256) {
+            sx[i] = traj[(long long)(base + i) * T * 2];
+            sy[i] = traj[(long long)(base + i) * T * 2 + 1];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int i = 0;
+            if (base == 0) { xs = sx[0]; ys = sy[0]; i = 1; }
+            for (; i < m; i++) {
+                xs = xs + sx[i];
+                ys = ys + sy[i];
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        double xm = (double)xs, ym = (double)ys;
+        xm /= N;
+        ym /= N;
+        s_mean[0] = (float)xm;
+        s_mean[1] = (float)ym;
+    }
+    __syncthreads();
+    const float xc = s_mean[0], yc = s_mean[1];
+    const int n = 2 * T;
+    for (long long e = tid; e < (long long)N * n; e += 256) {
+        const float v = traj[e];
+        const int r = (int)(e % n);
+        data[e] = (r % 2 == 0) ? v - xc : yc - v;
+    }
+}
+
+// Householder QR of the n x d sample and the last n - d columns of Q (see the oracle's
+// subspace_basis for the statement); A, V column-major with leading dimension n.
+__device__ void subspace_basis(double* A, int n, int d, double* V, double* beta, double* q2)
+{
+    for (int k = 0; k < d; k++) {
+        double nrm2 = 0.0;
+        for (int r = k; r < n; r++) nrm2 = nrm2 + A[k * n + r] * A[k * n + r];
+        const double nrm = __builtin_sqrt(nrm2);
+        const double x0 = A[k * n + k];
+        const double alpha = x0 >= 0.0 ? -nrm : nrm;
+        for (int r = k; r < n; r++) V[k * n + r] = A[k * n + r];
+        V[k * n + k] = x0 - alpha;
+        double b = 0.0;
+        for (int r = k; r < n; r++) b = b + V[k * n + r] * V[k * n + r];
+        beta[k] = b;
+        if (b == 0.0) continue;
+        for (int c = k; c < d; c++) {
+            double dot = 0.0;
+            for (int r = k; r < n; r++) dot = dot + V[k * n + r] * A[c * n + r];
+            const double f = 2.0 * dot / b;
+            for (int r = k; r < n; r++) A[c * n + r] = A[c * n + r] - f * V[k * n + r];
+        }
+    }
+    for (int j = d; j < n; j++) {
+        double* q = q2 + (j - d) * n;
+        for (int r = 0; r < n; r++) q[r] = r == j ? 1.0 : 0.0;
+        for (int k = d - 1; k >= 0; k--) {
+            if (beta[k] == 0.0) continue;
+            double dot = 0.0;
+            for (int r = k; r < n; r++) dot = dot + V[k * n + r] * q[r];
+            const double f = 2.0 * dot / beta[k];
+            for (int r = k; r < n; r++) q[r] = q[r] - f * V[k * n + r];
+        }
+    }
+}
+
+__device__ __forceinline__ double subspace_residual(const double* q2, int n, int m, const float* x)
+{
+    double res = 0.0;
+    for (int j = 0; j < m; j++) {
+        double p = 0.0;
+        for (int r = 0; r < n; r++) p = p + q2[j * n + r] * (double)x[r];
+        res = res + p * p;
+    }
+    return res;
+}
+
+// grid: one workgroup per hypothesis.  cols: [nhyp][d] sample indices; qbuf: [nhyp][n][n-d];
+// counts: [nhyp] inliers.
+__global__ __launch_bounds__(256) void k_subspace_hyp(const float* __restrict__ data, int N, int n, int d,
+                                                       const int* __restrict__ cols, double inlier_thr,
+                                                       double* __restrict__ qbuf, int* __restrict__ counts)
+{
+    __shared__ double sA[kMaxSub * kMaxSub], sV[kMaxSub * kMaxSub], sbeta[kMaxSub];
+    __shared__ double sq[kMaxSub * kMaxSub];
+    __shared__ int s_cnt[4];
+    const int h = blockIdx.x, tid = threadIdx.x, m = n - d;
+    for (int e = tid; e < n * d; e += 256) {
+        const int k = e / n, r = e - k * n;
+        sA[e] = (double)data[(long long)cols[h * d + k] * n + r];
+    }
+    __syncthreads();
+    if (tid == 0) subspace_basis(sA, n, d, sV, sbeta, sq);
+    __syncthreads();
+    for (int e = tid; e < n * m; e += 256) qbuf[(long long)h * n * m + e] = sq[e];
+    int cnt = 0;
+    for (int i = tid; i < N; i += 256)
+        if (subspace_residual(sq, n, m, data + (long long)i * n) < inlier_thr) cnt++;
+    for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if ((tid & 63) == 0) s_cnt[tid >> 6] = cnt;
+    __syncthreads();
+    if (tid == 0) counts[h] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+}
+
+// Winner = the first hypothesis with the largest positive count; its residual per trajectory and
+// the outlier flags.  best[0] = winner index or -1 (no hypothesis had an inlier).
+__global__ __launch_bounds__(256) void k_subspace_final(const float* __restrict__ data, int N, int n, int d,
+                                                         int nhyp, const int* __restrict__ counts,
+                                                         const double* __restrict__ qbuf, double out_thr,
+                                                         double* __restrict__ residuals,
+                                                         uint8_t* __restrict__ is_outlier, int* __restrict__ best)
+{
+    int bh = -1, bc = 0;
+    for (int h = 0; h < nhyp; h++)
+        if (counts[h] > bc) { bc = counts[h]; bh = h; }
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) best[0] = bh;
+    if (i >= N) return;
+    const int m = n - d;
+    double r = 0.0;
+    if (bh >= 0) r = subspace_residual(qbuf + (long long)bh * n * m, n, m, data + (long long)i * n);
+    if (residuals) residuals[i] = r;
+    is_outlier[i] = (uint8_t)(bh >= 0 && r > out_thr);
+}
+
+hipError_t launch_subspace(hipStream_t s, const float* traj, int N, int T, int d, const int* cols, int nhyp,
+                           double sigma, float* data, double* qbuf, int* counts, double* residuals,
+                           uint8_t* is_outlier, int* best)
+{
+    const int n = 2 * T;
+    // n - d == 10: the reference's chi_square_table.at(0).at(10) throws (outlier_detector.cpp:315)
+    if (N <= 0 || d <= 0 || d > n || n > kMaxSub || nhyp <= 0 || n - d == 10) return hipErrorInvalidValue;
+    const double inlier_thr = (double)(n - d) * sigma * sigma;
+    // chi-square 99% table (outlier_detector.cpp:19-30), indexed by n - d; 0.2 outside 1..10 (:311)
+    static const double p99[10] = {0.0, 0.020, 0.115, 0.297, 0.554, 0.872, 1.239, 1.646, 2.088, 2.558};
+    const double out_thr = (n - d > 0 && n - d < 10) ? sigma * sigma * p99[n - d] : 0.2;
+    hipLaunchKernelGGL(k_subspace_prep, dim3(1), dim3(256), 0, s, traj, N, T, data);
+    hipLaunchKernelGGL(k_subspace_hyp, dim3(nhyp), dim3(256), 0, s, data, N, n, d, cols, inlier_thr, qbuf, counts);
+    hipLaunchKernelGGL(k_subspace_final, dim3((N + 255) / 256), dim3(256), 0, s, data, N, n, d, nhyp, counts, qbuf,
+                       out_thr, residuals, is_outlier, best);
+    return hipGetLastError();
+}
+
+}  // namespace mdx

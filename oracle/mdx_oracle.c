@@ -884,3 +884,158 @@ int ora_flow_trajectory(const uint8_t* const* imgs, int nimg, int w, int h, int 
     free(cur); free(nxt); free(st); free(len); free(g1); free(g2);
     return num;
 }
+
+/* ----------------------------------------- trajectory subspace RANSAC - */
+/* glibc rand() (random_r TYPE_3: x[i] = x[i-3] + x[i-31], output x >> 1, after the 310-value
+ * warm-up srand does), the generator the reference draws its hypotheses from
+ * (outlier_detector.cpp:17 srand(time(NULL)), :226 rand() % cols).  Restated so runs are
+ * reproducible from a seed; pinned against this machine's libc in tests/test_subspace.py. */
+void ora_srand(ora_rand_state* s, uint32_t seed)
+{
+    int32_t r[34];
+    r[0] = (int32_t)(seed ? seed : 1);
+    for (int i = 1; i < 31; i++) {
+        const int64_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+        int64_t word = 16807 * lo - 2836 * hi;
+        if (word < 0) word += 2147483647;
+        r[i] = (int32_t)word;
+    }
+    for (int i = 31; i < 34; i++) r[i] = r[i - 31];
+    for (int i = 0; i < 34; i++) s->x[i] = (uint32_t)r[i];
+    s->i = 34;
+    for (int k = 0; k < 310; k++) (void)ora_rand(s);
+}
+
+int ora_rand(ora_rand_state* s)
+{
+    /* x[i] = x[i-31] + x[i-3] over a ring of 34 */
+    const int i = s->i;
+    const uint32_t v = s->x[(i - 31) % 34] + s->x[(i - 3) % 34];
+    s->x[i % 34] = v;
+    s->i = i + 1 >= 34 * 1024 ? (i + 1) % 34 + 34 : i + 1;
+    return (int)(v >> 1);
+}
+
+/* Householder QR of the n x d sample (double, column-major, LAPACK dgeqr2-style reflectors with
+ * beta = v'v) and the last n - d columns of Q = H_0 ... H_{d-1}: an orthonormal basis of the
+ * complement of the first d left singular vectors' span, i.e. Pnd = I - U_d U_d' = Q2 Q2'
+ * (outlier_detector.cpp:272-283; with a rank-deficient sample -- repeated indices -- the
+ * completion is implementation-defined there too).  Shared verbatim-in-order with the GPU
+ * kernel so both round identically.  q2: n x (n-d) column-major. */
+static void subspace_basis(double* A, int n, int d, double* q2)
+{
+    double V[ORA_MAX_SUBSPACE * ORA_MAX_SUBSPACE];   /* reflector k in column k (rows k..n-1) */
+    double beta[ORA_MAX_SUBSPACE];
+    for (int k = 0; k < d; k++) {
+        double nrm2 = 0.0;
+        for (int r = k; r < n; r++) nrm2 = nrm2 + A[k * n + r] * A[k * n + r];
+        const double nrm = sqrt(nrm2);
+        const double x0 = A[k * n + k];
+        const double alpha = x0 >= 0.0 ? -nrm : nrm;
+        for (int r = k; r < n; r++) V[k * n + r] = A[k * n + r];
+        V[k * n + k] = x0 - alpha;
+        double b = 0.0;
+        for (int r = k; r < n; r++) b = b + V[k * n + r] * V[k * n + r];
+        beta[k] = b;
+        if (b == 0.0) continue;
+        for (int c = k; c < d; c++) {            /* A[k:, c] -= 2 v (v'a) / b */
+            double dot = 0.0;
+            for (int r = k; r < n; r++) dot = dot + V[k * n + r] * A[c * n + r];
+            const double f = 2.0 * dot / b;
+            for (int r = k; r < n; r++) A[c * n + r] = A[c * n + r] - f * V[k * n + r];
+        }
+    }
+    for (int j = d; j < n; j++) {
+        double* q = q2 + (size_t)(j - d) * n;
+        for (int r = 0; r < n; r++) q[r] = r == j ? 1.0 : 0.0;
+        for (int k = d - 1; k >= 0; k--) {
+            if (beta[k] == 0.0) continue;
+            double dot = 0.0;
+            for (int r = k; r < n; r++) dot = dot + V[k * n + r] * q[r];
+            const double f = 2.0 * dot / beta[k];
+            for (int r = k; r < n; r++) q[r] = q[r] - f * V[k * n + r];
+        }
+    }
+}
+
+/* residual of one mean-subtracted trajectory column x (float, n): sum over the complement basis
+ * of (q' x)^2, in double, fixed order */
+static double subspace_residual(const double* q2, int n, int m, const float* x)
+{
+    double res = 0.0;
+    for (int j = 0; j < m; j++) {
+        double p = 0.0;
+        for (int r = 0; r < n; r++) p = p + q2[(size_t)j * n + r] * (double)x[r];
+        res = res + p * p;
+    }
+    return res;
+}
+
+/* meanSubtract (outlier_detector.cpp:200-221): float sums of row 0 / row 1 in column order,
+ * double mean, float constants; even rows minus the x mean, odd rows = y mean minus the row (the
+ * reference's y flip).  data: N columns of n floats (column i = trajectory i). */
+void ora_subspace_data(const float* traj, int N, int T, float* data)
+{
+    const int n = 2 * T;
+    float xs = 0.0f, ys = 0.0f;
+    for (int i = 0; i < N; i++) {
+        xs = i ? xs + traj[(size_t)i * T * 2] : traj[0];
+        ys = i ? ys + traj[(size_t)i * T * 2 + 1] : traj[1];
+    }
+    double xm = (double)xs, ym = (double)ys;
+    xm /= N;
+    ym /= N;
+    const float xc = (float)xm, yc = (float)ym;
+    for (int i = 0; i < N; i++)
+        for (int r = 0; r < n; r++) {
+            const float v = traj[(size_t)i * T * 2 + r];
+            data[(size_t)i * n + r] = (r % 2 == 0) ? v - xc : yc - v;
+        }
+}
+
+int ora_fit_subspace(const float* traj, int N, int T, int num_motions, double sigma, ora_rand_state* rng,
+                     int* columns, uint8_t* is_outlier, double* residuals)
+{
+    const int n = 2 * T, d = 4 * num_motions;
+    if (N <= 0 || d <= 0 || d > n || n > ORA_MAX_SUBSPACE || n - d == 10) return -1;
+    float* data = (float*)malloc(sizeof(float) * (size_t)N * n);
+    double* best_res = (double*)malloc(sizeof(double) * (size_t)N);
+    double* q2 = (double*)malloc(sizeof(double) * (size_t)n * (n - d > 0 ? n - d : 1));
+    double A[ORA_MAX_SUBSPACE * ORA_MAX_SUBSPACE];
+    int cols[ORA_MAX_SUBSPACE];
+    ora_subspace_data(traj, N, T, data);
+    const double inlier_thr = (double)(n - d) * sigma * sigma;
+    int max_points = 0, have = 0;
+    for (int it = 0; it < 50; it++) {
+        for (int k = 0; k < d; k++) {
+            cols[k] = ora_rand(rng) % N;
+            for (int r = 0; r < n; r++) A[k * n + r] = (double)data[(size_t)cols[k] * n + r];
+        }
+        subspace_basis(A, n, d, q2);
+        int np = 0;
+        for (int i = 0; i < N; i++)
+            if (subspace_residual(q2, n, n - d, data + (size_t)i * n) < inlier_thr) np++;
+        if (np > max_points) {
+            max_points = np;
+            have = 1;
+            for (int k = 0; k < d; k++) columns[k] = cols[k];
+            for (int i = 0; i < N; i++) best_res[i] = subspace_residual(q2, n, n - d, data + (size_t)i * n);
+        }
+    }
+    /* chi-square 99% table (:19-30), indexed by n - d */
+    static const double p99[10] = {0.0, 0.020, 0.115, 0.297, 0.554, 0.872, 1.239, 1.646, 2.088, 2.558};
+    double thr = 0.2;
+    if (n - d < 11 && n - d > 0) {
+        if (n - d == 10) { free(data); free(best_res); free(q2); return -1; }   /* vector::at(10) throws */
+        thr = sigma * sigma * p99[n - d];
+    }
+    int nout = 0;
+    for (int i = 0; i < N; i++) {
+        const int o = have && best_res[i] > thr;
+        if (is_outlier) is_outlier[i] = (uint8_t)o;
+        if (residuals) residuals[i] = have ? best_res[i] : 0.0;
+        nout += o;
+    }
+    free(data); free(best_res); free(q2);
+    return have ? nout : 0;
+}

@@ -109,6 +109,27 @@ int ora_flow_trajectory(const uint8_t* const* imgs, int nimg, int w, int h, int 
                         const ora_params* prm, int nthreads, float* traj, int* traj_len,
                         float* start_pts, double* vectors);
 
+/*
+ * Trajectory subspace RANSAC (OutlierDetector::fitSubspace, outlier_detector.cpp:236-331).
+ * traj: N trajectories of T points (x, y) (the complete ones of ora_flow_trajectory), n = 2T,
+ * d = 4*num_motions (d <= n <= ORA_MAX_SUBSPACE).  50 hypotheses of d columns drawn with
+ * ora_rand() % N; per hypothesis the residual of every trajectory against the complement of the
+ * sample's span; the first hypothesis with the most residuals < (n-d) sigma^2 wins.  Outputs:
+ * columns [d] (the winner's sample: the trajectories fitSubspace returns), is_outlier [N]
+ * (winner residual > sigma^2 * chi2_99[n-d], or 0.2 when n-d is outside 1..10; the reference
+ * reports trajectory[i][T-2] for each), residuals [N] (double).  Returns the outlier count
+ * (0 and columns untouched when no hypothesis has an inlier), -1 on bad arguments.
+ * Arithmetic: the reference's float meanSubtract, then double Householder QR + residuals (the
+ * reference uses Eigen's float JacobiSVD; see DESIGN.md for the parity statement).
+ */
+#define ORA_MAX_SUBSPACE 32
+typedef struct { uint32_t x[34]; int i; } ora_rand_state;
+void ora_srand(ora_rand_state* s, uint32_t seed);
+int  ora_rand(ora_rand_state* s);
+void ora_subspace_data(const float* traj, int N, int T, float* data);
+int  ora_fit_subspace(const float* traj, int N, int T, int num_motions, double sigma, ora_rand_state* rng,
+                      int* columns, uint8_t* is_outlier, double* residuals);
+
 /* Synthetic-frame generator spec is in the product (motion_detection_amd/csrc/synth.cpp);
  * the oracle does not need one. */
 

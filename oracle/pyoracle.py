@@ -32,6 +32,10 @@ class OraPyramid(C.Structure):
                 ("img", C.POINTER(C.c_uint8) * MAXL), ("deriv", C.POINTER(C.c_int16) * MAXL)]
 
 
+class OraRandState(C.Structure):
+    _fields_ = [("x", C.c_uint32 * 34), ("i", C.c_int)]
+
+
 def build(force: bool = False) -> str:
     """Compile the oracle with its Makefile (gcc is present on the GPU box too)."""
     src = os.path.join(_HERE, "mdx_oracle.c")
@@ -70,6 +74,14 @@ def lib():
         L.ora_flow_trajectory.argtypes = [C.POINTER(u8p), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                           C.POINTER(OraParams), C.c_int, f32p, C.POINTER(C.c_int), f32p, f64p]
         L.ora_flow_trajectory.restype = C.c_int
+        L.ora_srand.argtypes = [C.POINTER(OraRandState), C.c_uint32]
+        L.ora_srand.restype = None
+        L.ora_rand.argtypes = [C.POINTER(OraRandState)]
+        L.ora_rand.restype = C.c_int
+        L.ora_fit_subspace.argtypes = [f32p, C.c_int, C.c_int, C.c_int, C.c_double, C.POINTER(OraRandState),
+                                       C.POINTER(C.c_int), u8p, f64p]
+        L.ora_fit_subspace.restype = C.c_int
+        L.ora_subspace_data.argtypes = [f32p, C.c_int, C.c_int, f32p]
         _lib = L
     return _lib
 
@@ -223,3 +235,37 @@ def lk(gray1: np.ndarray, gray2: np.ndarray, prev_pts: np.ndarray, nthreads: int
     L.ora_free_pyramid(C.byref(P1))
     L.ora_free_pyramid(C.byref(P2))
     return nxt[:n], st[:n]
+
+
+def rand_state(seed: int) -> OraRandState:
+    """srand(seed) of the restated glibc generator."""
+    st = OraRandState()
+    lib().ora_srand(C.byref(st), seed & 0xFFFFFFFF)
+    return st
+
+
+def rand(st: OraRandState) -> int:
+    return lib().ora_rand(C.byref(st))
+
+
+def subspace_data(traj: np.ndarray) -> np.ndarray:
+    """meanSubtract (outlier_detector.cpp:200-221) of (N, T, 2) trajectories -> (N, 2T) float32."""
+    traj = np.ascontiguousarray(traj, dtype=np.float32)
+    N, T = traj.shape[:2]
+    out = np.zeros((N, 2 * T), np.float32)
+    lib().ora_subspace_data(_p(traj, C.c_float), N, T, _p(out, C.c_float))
+    return out
+
+
+def fit_subspace(traj: np.ndarray, num_motions: int, sigma: float, st: OraRandState):
+    """OutlierDetector::fitSubspace (outlier_detector.cpp:236-331).  Returns dict(n_outliers,
+    columns (d,), is_outlier (N,), residuals (N,)); n_outliers -1 on bad arguments."""
+    traj = np.ascontiguousarray(traj, dtype=np.float32)
+    N, T = traj.shape[:2]
+    d = 4 * num_motions
+    cols = np.full(d, -1, np.int32)
+    out = np.zeros(max(N, 1), np.uint8)
+    res = np.zeros(max(N, 1), np.float64)
+    n = lib().ora_fit_subspace(_p(traj, C.c_float), N, T, num_motions, sigma, C.byref(st),
+                               cols.ctypes.data_as(C.POINTER(C.c_int)), _p(out, C.c_uint8), _p(res, C.c_double))
+    return dict(n_outliers=n, columns=cols, is_outlier=out[:N], residuals=res[:N])
