@@ -247,6 +247,47 @@ def main_c4(args, D: Dist, threads: int):
     D.close()
 
 
+def live_leg(dev, w, h, threads, with_cpu=True, reps=5):
+    """The node's live chain (node.cpp:241-348): calculateOpticalFlowTrajectory
+    over 2*num_motions+1 = 5 rgb8 frames, then fitSubspace(num_motions 2, sigma 0.5) on the complete
+    trajectories.  Host-buffer entries, so the trajectory time includes the 5 frames' H2D."""
+    import ctypes as C
+    a, b, _ = mdx.synth_pair(SEED0 + 5, w, h, 3, threads)
+    frames = [a, b, a, b, a]          # the generator's pair, back and forth: every pass tracks
+    ctx = mdx.Context(dev, w, h, 4, pixel_step=10, min_vector_size=1.0)
+    rng = mdx._lib.MdxRandState()
+    mdx.lib().mdx_srand(C.byref(rng), SEED0)
+    res = ctx.flow_trajectory(frames)
+    traj = np.ascontiguousarray(np.array(res.trajectories, np.float32))
+    ctx.fit_subspace(traj, 2, 0.5, rng)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res = ctx.flow_trajectory(frames)
+    t1 = time.perf_counter()
+    traj = np.ascontiguousarray(np.array(res.trajectories, np.float32))
+    t2 = time.perf_counter()
+    for _ in range(reps):
+        sub = ctx.fit_subspace(traj, 2, 0.5, rng)
+    t3 = time.perf_counter()
+    ctx.close()
+    out = dict(workload=f"5 x {w}x{h} rgb8 frames, pixel_step 10: mdx_flow_trajectory + mdx_fit_subspace "
+                        f"(num_motions 2, sigma 0.5, 50 hypotheses)",
+               trajectory_ms=round((t1 - t0) / reps * 1e3, 3), fit_subspace_ms=round((t3 - t2) / reps * 1e3, 3),
+               points=int(len(res.traj_len)), complete_trajectories=int(len(traj)),
+               outliers=int(sub.is_outlier.sum()), includes="H2D of the frames (PCIe), D2H of the outputs")
+    if with_cpu:
+        from oracle import pyoracle   # CPU baseline leg only (test infrastructure)
+        c0 = time.perf_counter()
+        r = pyoracle.flow_trajectory(frames, nthreads=threads, pixel_step=10)
+        c1 = time.perf_counter()
+        pyoracle.fit_subspace(np.ascontiguousarray(np.array(r["trajectories"], np.float32)), 2, 0.5,
+                              pyoracle.rand_state(SEED0))
+        c2 = time.perf_counter()
+        out["cpu_oracle"] = dict(trajectory_ms=round((c1 - c0) * 1e3, 1), fit_subspace_ms=round((c2 - c1) * 1e3, 1),
+                                 cores=threads, kind="port")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -266,6 +307,7 @@ def main():
     ap.add_argument("--workload", default="c1", choices=["c1", "c4"],
                     help="c1: batched 1080p stream shards (the metric's config); c4: 8K RGB row-tiled")
     ap.add_argument("--bands", type=int, default=0, help="c4: row bands (default: one per rank)")
+    ap.add_argument("--no-live", action="store_true", help="skip the node's live trajectory + RANSAC leg")
     args = ap.parse_args()
 
     D = Dist()
@@ -360,6 +402,9 @@ def main():
     cpu = None
     if D.world == 1 and not args.no_cpu:
         cpu = cpu_baseline(uniq, w, h, args.cpu_seconds, threads)
+    live = None
+    if D.world == 1 and not args.no_live and not args.only_roofline:
+        live = live_leg(D.local_rank, w, h, threads, with_cpu=not args.no_cpu)
 
     lk_share = stages["lk"] / stages["total"] if stages["total"] > 0 else None
     out = {
@@ -387,6 +432,7 @@ def main():
                             "bound": "valu/lds (exact-order float chains), not hbm",
                             "points_per_s": round(px_all / (w * h) * mdx.grid_count(w, h, ps) / el_max, 1)},
         "num_vectors_pair0": int(num[0]),
+        "live_path": live,
     }
     if D.rank == 0:
         print(json.dumps(out), flush=True)
