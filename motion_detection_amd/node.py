@@ -15,6 +15,13 @@ encoding, step, data).  Parameters mirror the node's ROS params (:29-44, :237-24
 
 Publishing is a callback: ``on_result(result)`` receives the FlowResult (vectors + mask),
 standing in for publishImage on ~optical_flow_image (:83-85).
+
+With ``live_chain=True`` the callback follows the reference's live branch instead (:266-348):
+every ring frame goes to calculateOpticalFlowTrajectory (:295, runOpticalFlowTrajectory
+:94-110); with egomotion and at least one complete trajectory, fitSubspace(trajectories,
+outlier_points, num_motions, sigma) follows (:341-348).  ``on_result`` then receives a LiveResult.
+The default (False) drives the pair path the north star names (runOpticalFlow, :76-92), the only
+one that produces the motion mask.
 """
 from __future__ import annotations
 
@@ -59,10 +66,20 @@ def to_rgb8(msg: Image) -> np.ndarray:
     return px[:, :, ::-1].copy() if msg.encoding == "bgr8" else px.copy()
 
 
+@dataclass
+class LiveResult:
+    """Outputs of the live branch (node.cpp:266-348) up to the clustering it hands them to."""
+    num_vectors: int
+    optical_flow_vectors: np.ndarray     # (h, w, 4) Vec4d image (runOpticalFlowTrajectory :97-99)
+    trajectories: list                   # complete trajectories, (T, 2) each
+    outlier_points: list                 # fitSubspace's (egomotion only)
+    subspace: list                       # fitSubspace's return value (egomotion only)
+
+
 class MotionDetectionNode:
     def __init__(self, params: dict | None = None, on_result: Callable | None = None, device: int = 0):
         self.params = {"pixel_step": 10, "min_vector_size": 1.0, "skip_frames": 1, "num_motions": 2,
-                       "egomotion": False, "use_all_frames": True}
+                       "egomotion": False, "use_all_frames": True, "sigma": 0.5, "live_chain": False}
         if params:
             self.params.update(params)
         self.on_result = on_result
@@ -71,6 +88,8 @@ class MotionDetectionNode:
         self.image_received = False
         self.frames_processed = 0
         self.ofc = OpticalFlowCalculator(device=device)
+        self.od = None                                    # OutlierDetector, created on first use
+        self._device = device
 
     @property
     def trajectory_size(self) -> int:
@@ -93,8 +112,31 @@ class MotionDetectionNode:
             self.image_received = True
         if not (self.params.get("use_all_frames", True) and self.image_received):
             return None
+        if self.params.get("live_chain", False):
+            return self.run_live_chain([to_rgb8(m) for m in self.raw_images])   # :266-295
         frames = [to_rgb8(m) for m in list(self.raw_images)[-2:]]   # :266-287
         return self.run_optical_flow(frames[0], frames[1])
+
+    def run_live_chain(self, images: list):
+        """runOpticalFlowTrajectory (node.cpp:94-110) then, with egomotion, fitSubspace (:341-348)."""
+        h, w = images[0].shape[:2]
+        vec = np.zeros((h, w, 4))                         # cv::Mat::zeros(rows, cols, CV_32FC4) (:97)
+        trajectories: list = []
+        num = self.ofc.calculateOpticalFlowTrajectory(images, vec, trajectories, int(self.params["pixel_step"]),
+                                                      None, float(self.params["min_vector_size"]))
+        outliers: list = []
+        subspace: list = []
+        if trajectories and self.params["egomotion"]:
+            if self.od is None:
+                from .outlier_detector import OutlierDetector
+                self.od = OutlierDetector(seed=self.params.get("seed"), device=self._device)
+            subspace = self.od.fitSubspace(trajectories, outliers, int(self.params["num_motions"]),
+                                           float(self.params["sigma"]))
+        self.frames_processed += 1
+        res = LiveResult(num, vec, trajectories, outliers, subspace)
+        if self.on_result is not None:
+            self.on_result(res)
+        return res
 
     def run_optical_flow(self, image1: np.ndarray, image2: np.ndarray):
         """runOpticalFlow (node.cpp:76-92)."""

@@ -142,3 +142,44 @@ def test_calculate_optical_flow_no_vectors_leaves_comp(oracle):
     assert np.all(comp == 7)                              # :118 no mask branch: comp untouched
     pts = grid_points(64, 48, 8).astype(int)
     assert np.all(vec[pts[:, 1], pts[:, 0], :2] == -1)
+
+
+class RecordingLive:
+    """Stand-ins for the trajectory calculator and the detector (GPU work is tested elsewhere)."""
+    def __init__(self):
+        self.traj_calls, self.fit_calls = [], []
+
+    def calculateOpticalFlowTrajectory(self, images, vec, trajectories, pixel_step, comp, mvs):
+        self.traj_calls.append(([im.copy() for im in images], pixel_step, mvs))
+        trajectories.extend([np.zeros((len(images), 2), np.float32)] * 3)
+        return 7
+
+    def fitSubspace(self, trajectories, outlier_points, num_motions, sigma):
+        self.fit_calls.append((len(trajectories), num_motions, sigma))
+        outlier_points.append((1.0, 2.0))
+        return trajectories[:1]
+
+
+def test_live_chain_trajectory_and_subspace():
+    """Live branch (node.cpp:266-348): all ring frames to the trajectory call; with egomotion,
+    fitSubspace on its complete trajectories with num_motions and sigma."""
+    n = MotionDetectionNode({"egomotion": True, "num_motions": 2, "sigma": 0.7, "live_chain": True})
+    rec = RecordingLive()
+    n.ofc = rec
+    n.od = rec
+    for v in range(4):
+        assert n.image_callback(frame(v)) is None
+    res = n.image_callback(frame(4))
+    imgs, ps, mvs = rec.traj_calls[0]
+    assert [im[0, 0, 0] for im in imgs] == [0, 1, 2, 3, 4] and imgs[0].shape == (6, 8, 3)
+    assert (ps, mvs) == (10, 1.0)
+    assert rec.fit_calls == [(3, 2, 0.7)]
+    assert res.num_vectors == 7 and res.outlier_points == [(1.0, 2.0)] and len(res.subspace) == 1
+    # without egomotion: trajectories only (the reference clusters them instead, out of scope)
+    n2 = MotionDetectionNode({"live_chain": True})
+    rec2 = RecordingLive()
+    n2.ofc = rec2
+    n2.od = rec2
+    n2.image_callback(frame(1))
+    r2 = n2.image_callback(frame(2))
+    assert len(rec2.traj_calls[0][0]) == 2 and rec2.fit_calls == [] and r2.outlier_points == []
