@@ -308,6 +308,7 @@ def main():
                     help="c1: batched 1080p stream shards (the metric's config); c4: 8K RGB row-tiled")
     ap.add_argument("--bands", type=int, default=0, help="c4: row bands (default: one per rank)")
     ap.add_argument("--no-live", action="store_true", help="skip the node's live trajectory + RANSAC leg")
+    ap.add_argument("--no-4k", action="store_true", help="skip the whole-path 4K leg (config C2)")
     args = ap.parse_args()
 
     D = Dist()
@@ -325,7 +326,7 @@ def main():
                                   SEED0 + 1000 * D.rank, threads)
     if args.only_roofline:
         B, unique = 1, 1
-    ctx = mdx.Context(D.local_rank, w, h, B, pixel_step=ps, min_vector_size=1.0)
+    ctx = open_ctx(D, w, h, B, pixel_step=ps, min_vector_size=1.0)
     d1, d2 = ctx.dev_alloc(g1.nbytes), ctx.dev_alloc(g2.nbytes)
     dmask = ctx.dev_alloc(B * w * h)
     dnum = ctx.dev_alloc(B * 4)
@@ -361,6 +362,36 @@ def main():
         ctx.dev_free(p)
     del g1, g2
 
+    # ---- the whole path at 4K (config C2; the metric names 1080p & 4K): 8 pairs per step
+    full4k = None
+    if not args.no_4k and not args.only_roofline and args.config == "1080p":
+        kw, kh = CONFIGS["4k"]
+        KB = 8
+        k1, k2, _, _ = make_batch(kw, kh, KB, min(4, KB), SEED0 + 500 + 1000 * D.rank, threads)
+        kctx = open_ctx(D, kw, kh, KB, pixel_step=ps, min_vector_size=1.0)
+        f1, f2, fm = kctx.dev_alloc(k1.nbytes), kctx.dev_alloc(k2.nbytes), kctx.dev_alloc(KB * kw * kh)
+        kctx.h2d(f1, k1); kctx.h2d(f2, k2)
+
+        def step4k():
+            kctx.flow_warp_diff_batch_dev(KB, f1, f2, kw, kh, kw, kw * kh, mdx.FMT_GRAY8, d_mask=fm)
+
+        for _ in range(max(1, args.warmup)):
+            step4k()
+        kctx.device_sync()
+        D.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step4k()
+        kctx.device_sync()
+        D.barrier()
+        rate4k, el4k = throughput(D, float(args.steps * KB * kw * kh), time.perf_counter() - t0)
+        full4k = dict(workload=f"{kw}x{kh} gray pairs, whole reference path (max_level 5 -> 5 levels)", batch_per_gpu=KB,
+                      value=round(rate4k / 1e6, 2), unit="Mpixels/s", ms_per_step=round(el4k / args.steps * 1e3, 3))
+        for p in (f1, f2, fm):
+            kctx.dev_free(p)
+        kctx.close()
+        del k1, k2
+
     # ---- north-star kernel: fused warp+diff at 4K with the generator's true H
     roof = None
     if not args.no_roofline:
@@ -368,7 +399,7 @@ def main():
         RB = args.roofline_batch
         r1, r2, Hr, _ = make_batch(rw, rh, RB, min(4, RB), SEED0 + 77 + 1000 * D.rank, threads)
         Hb = np.ascontiguousarray(np.broadcast_to(Hr, (RB, 3, 3)), dtype=np.float64)
-        rctx = mdx.Context(D.local_rank, 64, 64, 1)   # warp-only: no pyramid workspace needed
+        rctx = open_ctx(D, 64, 64, 1)   # warp-only: no pyramid workspace needed
         e1, e2 = rctx.dev_alloc(r1.nbytes), rctx.dev_alloc(r2.nbytes)
         eH, eM = rctx.dev_alloc(Hb.nbytes), rctx.dev_alloc(RB * rw * rh)
         rctx.h2d(e1, r1); rctx.h2d(e2, r2); rctx.h2d(eH, Hb)
@@ -432,6 +463,7 @@ def main():
                             "bound": "valu/lds (exact-order float chains), not hbm",
                             "points_per_s": round(px_all / (w * h) * mdx.grid_count(w, h, ps) / el_max, 1)},
         "num_vectors_pair0": int(num[0]),
+        "full_path_4k": full4k,
         "live_path": live,
     }
     if D.rank == 0:

@@ -240,3 +240,36 @@ def test_row_tiled_matches_full(mdx, w, h, ps, nb, ch):
     assert int(out["num"][0]) == full.num_vectors == int(recs["count"].sum())
     np.testing.assert_array_equal(out["H"].view(np.uint64), full.H.view(np.uint64))
     assert int((out["mask"] != full.mask).sum()) == 0
+
+
+def test_full_path_4k_bit_exact(mdx, oracle):
+    """Config C2 (3840x2160, 5 pyramid levels) through the batched device entry, 2 pairs: every
+    output equals the oracle's (the bench's full_path_4k leg runs this path)."""
+    w, h, B = 3840, 2160, 2
+    pairs = [mdx.synth_pair(40 + i, w, h, 1) for i in range(B)]
+    g1 = np.stack([p[0] for p in pairs]); g2 = np.stack([p[1] for p in pairs])
+    n = mdx.grid_count(w, h, 10)
+    with mdx.Context(0, w, h, B, pixel_step=10, min_vector_size=1.0) as c:
+        bufs = [c.dev_alloc(x) for x in (g1.nbytes, g2.nbytes, B * n * 8, B * n, B * n * 32, B * w * h, B * 72, B * 4)]
+        try:
+            c.h2d(bufs[0], g1); c.h2d(bufs[1], g2)
+            c.flow_warp_diff_batch_dev(B, bufs[0], bufs[1], w, h, w, w * h, mdx.FMT_GRAY8, d_next_pts=bufs[2],
+                                       d_status=bufs[3], d_vectors=bufs[4], d_mask=bufs[5], d_H=bufs[6],
+                                       d_num_vectors=bufs[7])
+            c.sync()
+            npts = np.empty((B, n, 2), np.float32); st = np.empty((B, n), np.uint8)
+            vec = np.empty((B, n, 4)); mask = np.empty((B, h, w), np.uint8)
+            H = np.empty((B, 9)); num = np.empty(B, np.int32)
+            for arr, p in zip((npts, st, vec, mask, H, num), bufs[2:]):
+                c.d2h(arr, p)
+        finally:
+            for p in bufs:
+                c.dev_free(p)
+    for i in range(B):
+        ref = oracle.calculate_optical_flow(g1[i], g2[i], nthreads=16, pixel_step=10, min_vector_size=1.0)
+        assert num[i] == ref["num_vectors"]
+        np.testing.assert_array_equal(st[i], ref["status"])
+        np.testing.assert_array_equal(npts[i].view(np.uint32), ref["next_pts"].view(np.uint32))
+        np.testing.assert_array_equal(vec[i], ref["vectors"])
+        np.testing.assert_array_equal(H[i].view(np.uint64), ref["H"].ravel().view(np.uint64))
+        assert int((mask[i] != ref["mask"]).sum()) == 0, f"pair {i}"
