@@ -471,7 +471,9 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
     mark(c, 1);
     for (int l = 1; l < g.nlev; l++) HIP_OR_RETURN(c, launch_pyrdown(s, batch, pyr1, pyr2, g, l));
     mark(c, 2);
-    for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, batch, pyr1, der, g, l));
+    // Scharr derivatives feed only the LK.  The class-plane LK launches them itself, on its
+    // aux stream right before each level's class planes, so they overlap the coarser levels'
+    // iterations; the single-kernel LK needs them up front.
     mark(c, 3);
     if (npts > 0 && nyb > 0) {
         LkArgs a{};
@@ -498,6 +500,7 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         if (!v2) {
             if (gy0 != 0 || gy1 != ny)
                 return set_err(c, MDX_EINVAL, "row bands need the class-plane LK (pixel_step too large)");
+            for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, batch, pyr1, der, g, l));
             HIP_OR_RETURN(c, launch_lk(s, batch, a));
         } else {
             a.plan = c->plan;

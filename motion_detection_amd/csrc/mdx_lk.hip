@@ -722,6 +722,9 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             ca.rlist = a.rlist;
             ca.level = l;
             const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.vhi - C.vlo, nb * C.nrx * C.nry);
+            // this level's Scharr planes (the caller left them to us): on the aux stream, so they
+            // too run while the coarser levels iterate
+            if (hipError_t e = launch_scharr(sa, nb, b.pyr1, const_cast<uint32_t*>(b.der), a.g, l)) return e;
             hipLaunchKernelGGL(k_lk_class, grid, dim3(64), 0, sa, b.pyr1, b.der, bcls, ca);
             float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             const int G = C.G, UW = C.UW;
