@@ -347,8 +347,11 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
         for (int gi = 0; gi < 10; gi++) {
             const uint32_t d = ld[4 * gi];
             const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
-            sd = sd + f * f;                 // (Ix*Ix, Iy*Iy)
-            s12 = s12 + f.x * f.y;           // Ix*Iy
+            // the reference rounds each product to float, then adds (_mm_mul_ps, _mm_add_ps).
+            // |Ix|, |Iy| <= 4080 (Scharr of u8, interpolated), so every product is below 2^24 and
+            // exact in float: one fused multiply-add rounds exactly like the two operations
+            sd = __builtin_elementwise_fma(f, f, sd);      // (Ix*Ix, Iy*Iy)
+            s12 = __builtin_fmaf(f.x, f.y, s12);           // Ix*Iy
         }
         if (y + 1 < kWin) {
             lstore(buf ^ 1, rq[y % PF]);     // row y+1

@@ -10,7 +10,7 @@ mkdir -p ../build/var
 for v in "$@"; do
     name=${v%%:*}; defs=${v#*:}
     $H $F $defs -c mdx_lk.hip -o ../build/var/lk_$name.o
-    $H --offload-arch=gfx950 -shared -fPIC -pthread ../build/mdx_kernels.o ../build/var/lk_$name.o ../build/mdx_warp.o ../build/mdx_api.o \
+    $H --offload-arch=gfx950 -shared -fPIC -pthread ../build/mdx_kernels.o ../build/var/lk_$name.o ../build/mdx_warp.o ../build/mdx_subspace.o ../build/mdx_api.o \
         ../build/synth.o -o ../lib/libmdx_$name.so
     echo "built libmdx_$name.so ($defs)"
 done
