@@ -516,9 +516,18 @@ __device__ double dev_hypot(double x, double y)
 // getPerspectiveTransform(src, dst) = solve(A, b, DECOMP_SVD) on the 8x8 DLT system:
 // lapack.cpp JacobiSVDImpl_<double> (one-sided Jacobi on A's columns, eps 10*DBL_EPSILON,
 // max(m,30) sweeps, descending sort) then SVBkSb (threshold 2*DBL_EPSILON*sum(w)).
-__device__ void dev_perspective_fit(const float* src, const float* dst, double* M)
-{
+// The working arrays live in LDS (one lane runs the solve): as private arrays they were
+// scratch memory, whose latency every dependent step of the sweep paid.
+struct FitWork {
     double At[64], Vt[64], W[8], bv[8], x[8];
+};
+__device__ __forceinline__ void dev_perspective_fit(const float* src, const float* dst, double* M, FitWork& fw)
+{
+    double* At = fw.At;
+    double* Vt = fw.Vt;
+    double* W = fw.W;
+    double* bv = fw.bv;
+    double* x = fw.x;
     for (int i = 0; i < 64; i++) At[i] = 0.0;
     for (int i = 0; i < 4; i++) {
         const float sx = src[2 * i], sy = src[2 * i + 1], dx = dst[2 * i], dy = dst[2 * i + 1];
@@ -725,6 +734,7 @@ __global__ __launch_bounds__(64) void k_fit(const float* __restrict__ next_pts, 
         carry += __shfl(incl, 63);
     }
     if (lane != 0) return;
+    __shared__ FitWork fw;
     PairFit& f = fits[pair];
     const int total = carry;
     f.num_vectors = total;
@@ -742,7 +752,7 @@ __global__ __launch_bounds__(64) void k_fit(const float* __restrict__ next_pts, 
             dst[2 * r] = e.x;
             dst[2 * r + 1] = e.y;
         }
-        dev_perspective_fit(src, dst, f.H);
+        dev_perspective_fit(src, dst, f.H, fw);
         dev_invert3x3(f.H, f.Hinv);
         f.fit_status = 0;
     } else {
@@ -831,8 +841,9 @@ __global__ void k_band_fit(const mdx_band_cand* __restrict__ cands, int nrec, Pa
     }
     PairFit& f = *fit;
     f.num_vectors = total;
+    __shared__ FitWork fw;
     if (total >= 4) {
-        dev_perspective_fit(bs, bd, f.H);
+        dev_perspective_fit(bs, bd, f.H, fw);
         dev_invert3x3(f.H, f.Hinv);
         f.fit_status = 0;
     } else {
