@@ -36,12 +36,15 @@
 // dot2(pa, W0, dot2(pb, W1, C)) >> 9 == ((S + 256) >> 9) - I exactly, because C = 256 - 512*I
 // is a multiple-of-512 shift of the rounding bias.  Products are float multiplies of exactly
 // converted integers (one rounding of the exact product == the reference's (float)(int
-// product)).  Products/sums never go through FMA (-ffp-contract=off).
+// product)).  Products/sums never go through a contracted FMA (-ffp-contract=off); k_lk_A's
+// explicit FMAs multiply operands whose product is exact in float (|Ix|, |Iy| <= 4080), so they
+// round like the separate multiply and add.
 #include "mdx_internal.h"
 
 #include <float.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -645,19 +648,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER
     }
 }
 
-// persistent waves for k_lk_iter: what the device keeps resident at once
+// persistent waves for k_lk_iter: what the current device keeps resident at once (cached per
+// device; contexts on several devices may launch from several host threads)
 template <int G, int UW>
 static int lk_iter_resident()
 {
-    static int cached = 0;
-    if (!cached) {
-        int dev = 0, ncu = 0, nb = 0;
-        (void)hipGetDevice(&dev);
+    constexpr int kDevs = 64;
+    static std::atomic<int> cached[kDevs];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int v = dev >= 0 && dev < kDevs ? cached[dev].load(std::memory_order_relaxed) : 0;
+    if (!v) {
+        int ncu = 0, nb = 0;
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lk_iter<G, UW>, 64, 0);
-        cached = std::max(1, ncu) * std::max(1, nb);
+        v = std::max(1, ncu) * std::max(1, nb);
+        if (dev >= 0 && dev < kDevs) cached[dev].store(v, std::memory_order_relaxed);
     }
-    return cached;
+    return v;
 }
 
 template <int G, int UW>
