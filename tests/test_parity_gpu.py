@@ -32,6 +32,15 @@ CASES = [
     (333, 241, 7, 1, 11),
     (320, 240, 10, 3, 5),
     (1920, 1080, 10, 1, 20141106),
+    # dense and sparse grids, frames at the pyramid's 40-px limits: pixel_step 1 (every pixel a
+    # point, the step where the reference's Vec4d writes overflow), 2, 4, 16, 40, 64
+    (81, 83, 1, 1, 31),
+    (41, 41, 1, 1, 36),
+    (64, 41, 2, 1, 32),
+    (200, 150, 4, 1, 33),
+    (200, 150, 16, 1, 34),
+    (210, 160, 40, 1, 35),
+    (1920, 1080, 64, 1, 37),
 ]
 
 
