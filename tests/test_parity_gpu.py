@@ -208,7 +208,7 @@ def test_reference_interface(mdx, oracle):
 
 
 @pytest.mark.parametrize("w,h,ps,nb,ch", [(640, 480, 10, 3, 1), (333, 241, 7, 5, 1), (1920, 1080, 10, 8, 1),
-                                          (640, 480, 3, 2, 3), (320, 240, 10, 1, 1)])
+                                          (640, 480, 3, 2, 3), (320, 240, 10, 1, 1), (7680, 4320, 10, 8, 3)])
 def test_row_tiled_matches_full(mdx, w, h, ps, nb, ch):
     """Row bands run one after another on one GPU, records exchanged through
     host memory: every point, the fit, the count and every mask row equal the full path's."""
@@ -282,3 +282,14 @@ def test_full_path_4k_bit_exact(mdx, oracle):
         np.testing.assert_array_equal(vec[i], ref["vectors"])
         np.testing.assert_array_equal(H[i].view(np.uint64), ref["H"].ravel().view(np.uint64))
         assert int((mask[i] != ref["mask"]).sum()) == 0, f"pair {i}"
+
+
+def test_full_path_8k_rgb_bit_exact(mdx, oracle):
+    """Config C4's frame (7680x4320 rgb8, 6 pyramid levels 0..5) on one GPU: every output equals
+    the oracle's (the row-tiled form is checked against this path above)."""
+    w, h = 7680, 4320
+    a, b, _ = mdx.synth_pair(4242, w, h, 3)
+    with mdx.Context(0, w, h, 1, pixel_step=10, min_vector_size=1.0) as c:
+        res = c.flow_warp_diff(a, b, fmt=mdx.FMT_RGB8)
+    ref = oracle.calculate_optical_flow(a, b, fmt=oracle.FMT_RGB8, nthreads=16, pixel_step=10, min_vector_size=1.0)
+    _compare(res, ref, "8k rgb")
