@@ -508,7 +508,7 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
             a.rlist = c->ctab.as<int16_t>() + kMaxLevels * 2 * 128;
             a.ord = c->ctab.as<int16_t>() + 2 * kMaxLevels * 2 * 128;
             if (c->lk_debug) {
-                if ((rc = ensure(c, c->dbg, ((size_t)npts * g.nlev * batch + kMaxLevels * 64) * 16)) != MDX_OK)
+                if ((rc = ensure(c, c->dbg, ((size_t)npts * g.nlev * batch + kLkDbgStampOff + kMaxLevels * kLkDbgWaves) * 16)) != MDX_OK)
                     return rc;
                 a.dbg = c->dbg.as<float4>();
                 const char* e = std::getenv("MDX_LK_DEBUG_PT");

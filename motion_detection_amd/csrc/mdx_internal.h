@@ -10,6 +10,11 @@
 namespace mdx {
 
 constexpr int kMaxLevels = 8;
+// LK debug buffer (MDX_LK_DEBUG=1): after the per-point records, the traced point's iterations
+// (kMaxLevels * 64 float4), then per level and persistent wave of k_lk_iter its {start, end}
+// s_memrealtime stamps (100 MHz), for the wave-occupancy profile (scripts/lk_tail.py)
+constexpr int kLkDbgStampOff = kMaxLevels * 64 + 64;
+constexpr int kLkDbgWaves = 16384;
 constexpr int kWin = 40;     // LK window side (reference optical_flow_calculator.cpp:41)
 constexpr int kPad = 40;     // border rows/cols every pyramid level carries (= win)
 constexpr int kXOff = 64;    // left margin of a level row: the core starts 64-B aligned

@@ -409,6 +409,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER
 
     const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
     const unsigned long long smask = ((1ull << LPS) - 1) << (slot * LPS);
+    const unsigned long long t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int xcd = blockIdx.x & 7;
     const long long T = (long long)batch * ngroups;
     const long long cb = T * xcd / 8, ce = T * (xcd + 1) / 8;     // this XCD's range of the work list
@@ -645,6 +646,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER
                 retire();
             }
         }
+    }
+    if (a.dbg && lane == 0 && blockIdx.x < kLkDbgWaves) {   // debug mode only: wave lifetimes
+        uint4* st = reinterpret_cast<uint4*>(a.dbg + (long long)batch * a.g.nlev * a.npts + kLkDbgStampOff) +
+                    (long long)level * kLkDbgWaves + blockIdx.x;
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        *st = make_uint4((uint32_t)t_start, (uint32_t)(t_start >> 32), (uint32_t)t_end, (uint32_t)(t_end >> 32));
     }
 }
 
