@@ -437,6 +437,49 @@ static inline void mark(mdx_ctx* c, int i)
     if (c->cur >= 0) (void)hipEventRecord(c->ev[c->cur * 7 + i], c->stream);
 }
 
+// The LK of a batch of pairs on the context's stream.  Grid start points (a.prev_pts null) on a
+// dense enough grid take the class-plane kernels, which launch each level's Scharr planes
+// themselves; otherwise the single kernel, after the Scharr planes unless the caller already
+// computed them (have_scharr).  a: every field but the class-plan ones.
+static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, int h, int gy0, int gy1,
+                  bool have_scharr)
+{
+    int rc;
+    hipStream_t s = c->stream;
+    bool v2 = c->lk_impl == 2 && a.prev_pts == nullptr;
+    if (v2) {
+        if ((rc = ensure_class_plan(c, g, w, h, c->prm.pixel_step, batch, gy0, gy1)) != MDX_OK) return rc;
+        v2 = c->plan.nch != 0;   // very sparse grids: the single-kernel LK
+    }
+    if (!v2) {
+        if (gy0 != 0 || gy1 != a.ny)
+            return set_err(c, MDX_EINVAL, "row bands need the class-plane LK (pixel_step too large)");
+        if (!have_scharr)
+            for (int l = 0; l < g.nlev; l++)
+                HIP_OR_RETURN(c, launch_scharr(s, batch, a.pyr1, const_cast<uint32_t*>(a.der), g, l));
+        HIP_OR_RETURN(c, launch_lk(s, batch, a));
+        return MDX_OK;
+    }
+    a.plan = c->plan;
+    a.cmap = c->ctab.as<int16_t>();
+    a.rlist = c->ctab.as<int16_t>() + kMaxLevels * 2 * 128;
+    a.ord = c->ctab.as<int16_t>() + 2 * kMaxLevels * 2 * 128;
+    const int npts = a.npts;
+    if (c->lk_debug) {
+        if ((rc = ensure(c, c->dbg, ((size_t)npts * g.nlev * batch + kLkDbgStampOff + kMaxLevels * kLkDbgWaves) * 16)) !=
+            MDX_OK)
+            return rc;
+        a.dbg = c->dbg.as<float4>();
+        const char* e = std::getenv("MDX_LK_DEBUG_PT");
+        a.dbg_pt = e ? std::atoi(e) : -1;
+    }
+    const size_t abytes = (size_t)g.nlev * batch * npts * sizeof(float4);
+    if ((rc = ensure(c, c->Abuf, abytes + (size_t)batch * kMaxLevels * 8 * sizeof(int))) != MDX_OK) return rc;
+    HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
+                                  reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes)));
+    return MDX_OK;
+}
+
 // The pipeline on device buffers.  d_np/d_st must be valid (LK writes them).
 // Row-band mode (cand != null, batch 1): LK and classification for grid rows [gy0, gy1) only, the
 // band's record to *cand, no fit and no mask.
@@ -492,33 +535,7 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         a.eps2 = e * e;
         a.next_pts = d_np;
         a.status = d_st;
-        bool v2 = c->lk_impl == 2;
-        if (v2) {
-            if ((rc = ensure_class_plan(c, g, w, h, P.pixel_step, batch, gy0, gy1)) != MDX_OK) return rc;
-            v2 = c->plan.nch != 0;   // very sparse grids: the single-kernel LK
-        }
-        if (!v2) {
-            if (gy0 != 0 || gy1 != ny)
-                return set_err(c, MDX_EINVAL, "row bands need the class-plane LK (pixel_step too large)");
-            for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, batch, pyr1, der, g, l));
-            HIP_OR_RETURN(c, launch_lk(s, batch, a));
-        } else {
-            a.plan = c->plan;
-            a.cmap = c->ctab.as<int16_t>();
-            a.rlist = c->ctab.as<int16_t>() + kMaxLevels * 2 * 128;
-            a.ord = c->ctab.as<int16_t>() + 2 * kMaxLevels * 2 * 128;
-            if (c->lk_debug) {
-                if ((rc = ensure(c, c->dbg, ((size_t)npts * g.nlev * batch + kLkDbgStampOff + kMaxLevels * kLkDbgWaves) * 16)) != MDX_OK)
-                    return rc;
-                a.dbg = c->dbg.as<float4>();
-                const char* e = std::getenv("MDX_LK_DEBUG_PT");
-                a.dbg_pt = e ? std::atoi(e) : -1;
-            }
-            const size_t abytes = (size_t)g.nlev * batch * npts * sizeof(float4);
-            if ((rc = ensure(c, c->Abuf, abytes + (size_t)batch * kMaxLevels * 8 * sizeof(int))) != MDX_OK) return rc;
-            HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
-                                          reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes)));
-        }
+        if ((rc = run_lk(c, g, a, batch, w, h, gy0, gy1, false)) != MDX_OK) return rc;
     }
     mark(c, 4);
     if ((rc = ensure(c, c->csum, classify_scratch_bytes(batch, npts))) != MDX_OK) return rc;
@@ -680,8 +697,10 @@ extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int n
         a.eps2 = e * e;
         a.next_pts = c->tnp.as<float>();
         a.status = c->tst.as<uint8_t>();
-        a.prev_pts = cur;
-        HIP_OR_RETURN(c, launch_lk(s, 1, a));
+        // pass 0 starts on the grid: the class-plane LK when the grid allows it; later passes
+        // start where the previous one ended (the single-kernel LK)
+        a.prev_pts = j == 0 ? nullptr : cur;
+        if ((rc = run_lk(c, g, a, 1, w, h, 0, ny, true)) != MDX_OK) return rc;
         HIP_OR_RETURN(c, launch_traj_update(s, npts, c->tnp.as<float>(), c->tst.as<uint8_t>(), cur, tr, tl, nimg, w, h,
                                             j == npairs - 1, P.min_vector_size, c->tvec.as<double>(),
                                             c->tstart.as<float>(), dnum));
