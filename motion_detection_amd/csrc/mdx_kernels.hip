@@ -992,7 +992,9 @@ hipError_t launch_traj_update(hipStream_t s, int npts, const float* next_pts, co
 
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a)
 {
-    constexpr int LPP = 32, PPW = 64 / LPP;
+    // one point per wave: 124 VGPRs, 4 waves per SIMD (two points per wave took 172 VGPRs, 2 waves
+    // per SIMD, and ran the trajectory passes 1.5x slower)
+    constexpr int LPP = 64, PPW = 64 / LPP;
     const dim3 grid((a.npts + PPW - 1) / PPW, batch);
     hipLaunchKernelGGL(k_lk<LPP>, grid, dim3(64), 0, s, a);
     return hipGetLastError();
