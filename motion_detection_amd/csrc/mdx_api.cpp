@@ -697,9 +697,10 @@ extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int n
         a.eps2 = e * e;
         a.next_pts = c->tnp.as<float>();
         a.status = c->tst.as<uint8_t>();
-        // pass 0 starts on the grid: the class-plane LK when the grid allows it; later passes
-        // start where the previous one ended (the single-kernel LK)
-        a.prev_pts = j == 0 ? nullptr : cur;
+        // every pass on the single-kernel LK from the carried points: for one pair it is faster
+        // than the class-plane kernels even on the grid start points of pass 0 (live leg 4.7 vs
+        // 5.2 ms), whose per-level tails one pair cannot fill
+        a.prev_pts = cur;
         if ((rc = run_lk(c, g, a, 1, w, h, 0, ny, true)) != MDX_OK) return rc;
         HIP_OR_RETURN(c, launch_traj_update(s, npts, c->tnp.as<float>(), c->tst.as<uint8_t>(), cur, tr, tl, nimg, w, h,
                                             j == npairs - 1, P.min_vector_size, c->tvec.as<double>(),
