@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256) void k_subspace_prep(const float* __restrict__
                                                         float* __restrict__ data)
 {
     constexpr int kChunk = 4096;
-    __shared__ float sx[kChunk], sy[kChunk];
+    __shared__ __attribute__((aligned(16))) float sx[kChunk], sy[kChunk];
     __shared__ float s_mean[2];
     const int tid = threadIdx.x;
     float xs = 0.f, ys = 0.f;
@@ -40,8 +40,29 @@ __global__ __launch_bounds__(256) void k_subspace_prep(const float* __restrict__
         }
         __syncthreads();
         if (tid == 0) {
+            // the reference's order exactly (one float chain per axis); 16 values per axis are
+            // read ahead with ds_read_b128 so the chain waits on the adds, not on LDS latency
             int i = 0;
             if (base == 0) { xs = sx[0]; ys = sy[0]; i = 1; }
+            for (; i < m && (i & 3); i++) {
+                xs = xs + sx[i];
+                ys = ys + sy[i];
+            }
+            for (; i + 16 <= m; i += 16) {
+                float4 x4[4], y4[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    x4[k] = reinterpret_cast<const float4*>(sx + i)[k];
+                    y4[k] = reinterpret_cast<const float4*>(sy + i)[k];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    xs = xs + x4[k].x; ys = ys + y4[k].x;
+                    xs = xs + x4[k].y; ys = ys + y4[k].y;
+                    xs = xs + x4[k].z; ys = ys + y4[k].z;
+                    xs = xs + x4[k].w; ys = ys + y4[k].w;
+                }
+            }
             for (; i < m; i++) {
                 xs = xs + sx[i];
                 ys = ys + sy[i];
