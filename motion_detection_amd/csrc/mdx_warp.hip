@@ -156,6 +156,7 @@ __device__ TileInfo tile_info(const double* M, int x0, int y0, int w, int yend, 
 typedef __attribute__((address_space(3))) const uint8_t lds_u8;
 typedef __attribute__((address_space(3))) const uint32_t lds_u32;
 typedef double d2v __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const d2v lds_d2;
 
 // raw buffer descriptor over [base, base + bytes): out-of-range loads return 0 and stores are
@@ -251,6 +252,30 @@ __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t sr
     }
 }
 
+// staging: rows per pass and ceil(2^16 / nch) for nch = 1..16 chunks per footprint row
+__constant__ int kRowsPerPass[17] = {0, 256, 128, 85, 64, 51, 42, 36, 32, 28, 25, 23, 21, 19, 18, 17, 16};
+__constant__ uint32_t kInvChunks[17] = {0,     65536, 32768, 21846, 16384, 13108, 10923, 9363, 8192,
+                                        7282,  6554,  5958,  5462,  5042,  4682,  4370,  4096};
+
+// footprint chunks that cross the image's left / right edge: byte by byte, 0 outside (kept out of
+// line so its per-byte bounds are not computed on the interior path)
+__device__ __noinline__ void stage_edge_chunks(const uint8_t* src, int pitch, int w, int h, int sya, int sx, int ro,
+                                               int rpp, int sh, uint8_t* dst)
+{
+    for (int r = ro; r < sh; r += rpp) {
+        const int sy = sya + r;
+        uint32_t d[4] = {0, 0, 0, 0};
+        if ((unsigned)sy < (unsigned)h) {
+            const uint8_t* p = src + (long long)sy * pitch;
+            for (int i = 0; i < 16; i++) {
+                const int xx = sx + i;
+                if ((unsigned)xx < (unsigned)w) d[i >> 2] |= (uint32_t)p[xx] << (8 * (i & 3));
+            }
+        }
+        *reinterpret_cast<uint4*>(dst + r * kSP) = make_uint4(d[0], d[1], d[2], d[3]);
+    }
+}
+
 // grid: x -> tile column, y -> tile row of the band [row0, row1), z -> pair.  256 threads; lane l
 // of wave q owns columns x0 + 4*(l & 31) .. +3 of tile rows 2q + (l >> 5) + 8i, i = 0..7.  The
 // reference's blocking depends on the full height only through bw0, and each pixel's arithmetic
@@ -331,34 +356,29 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
         s_xy[r][b][1] = M[3] * xb + M[4] * y + M[5];
     }
     {
+        // lane -> (row, 16-B chunk) of the footprint without an integer division: ro = tid / nch
+        // as a multiply by ceil(2^16 / nch) (exact for tid < 4096)
         const int nch = (t.sw + 15) >> 4;                 // <= kSP / 16
-        const int rpp = 256 / nch;                        // rows per pass
-        const int ro = tid / nch, ch = tid - ro * nch;    // once per thread
+        const int rpp = kRowsPerPass[nch];                // 256 / nch rows per pass
+        const int ro = (int)(((uint32_t)tid * kInvChunks[nch]) >> 16), ch = tid - ro * nch;
         const int sx = t.sxa + 16 * ch;
-        const bool xin = sx >= 0 && sx + 16 <= w;
         if (ro < rpp) {
-            for (int r = ro; r < t.sh; r += rpp) {
-                const int sy = t.sya + r;
-                uint4 v;
+            if (sx >= 0 && sx + 16 <= w) {
+                // whole chunks inside the row: buffer loads, rows above / below the image fall
+                // outside the descriptor and read 0 (BORDER_CONSTANT)
+                const __amdgpu_buffer_rsrc_t srs = buf_rsrc(src, (long long)h * g1_pitch);
+                uint32_t off = (uint32_t)((t.sya + ro) * g1_pitch + sx);
+                const uint32_t step = (uint32_t)(rpp * g1_pitch);
+                for (int r = ro; r < t.sh; r += rpp, off += step) {
 #ifdef WX_NO_STAGE   // WX_*: timing-only builds (scripts/warp_variants.sh), results invalid
-                if (true) {
-                    v = make_uint4(sy, sx, r, ch);
+                    const v4u v = {(uint32_t)r, (uint32_t)sx, off, (uint32_t)ch};
 #else
-                if ((unsigned)sy < (unsigned)h && xin) {
-                    v = *reinterpret_cast<const uint4*>(src + (long long)sy * g1_pitch + sx);
+                    const v4u v = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)off, 0, 0);
 #endif
-                } else {
-                    uint32_t d[4] = {0, 0, 0, 0};
-                    if ((unsigned)sy < (unsigned)h) {
-                        const uint8_t* p = src + (long long)sy * g1_pitch;
-                        for (int i = 0; i < 16; i++) {
-                            const int xx = sx + i;
-                            if ((unsigned)xx < (unsigned)w) d[i >> 2] |= (uint32_t)p[xx] << (8 * (i & 3));
-                        }
-                    }
-                    v = make_uint4(d[0], d[1], d[2], d[3]);
+                    *reinterpret_cast<uint4*>(&s_src[r * kSP + 16 * ch]) = make_uint4(v.x, v.y, v.z, v.w);
                 }
-                *reinterpret_cast<uint4*>(&s_src[r * kSP + 16 * ch]) = v;
+            } else {
+                stage_edge_chunks(src, g1_pitch, w, h, t.sya, sx, ro, rpp, t.sh, &s_src[16 * ch]);
             }
         }
     }
