@@ -291,10 +291,10 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
     __shared__ TileInfo s_info;
 
-    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs; remap the linear id so
-    // each XCD walks a contiguous run of tiles (row-major), and horizontally adjacent tiles --
-    // which share the 128-B lines of their gray1 footprints and gray2 / mask rows -- meet in
-    // the same L2 at about the same time.
+    // Tile order: plain grid coordinates.  An XCD-aware remap (each XCD walking a contiguous run
+    // of tiles, WX_REMAP) measured no faster: a 128-px tile's gray2 / mask rows are whole 128-B
+    // lines, so neighbours share only the footprint margins, and the remap's divisions cost VALU.
+#ifdef WX_REMAP
     const int nbx = gridDim.x, nby = gridDim.y;
     int bid = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
     {
@@ -302,8 +302,12 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
         bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     }
     const int pair = bid / (nbx * nby), tile = bid - pair * (nbx * nby);
+    const int tx_ = tile % nbx, ty_ = tile / nbx;
+#else
+    const int pair = blockIdx.z, tx_ = blockIdx.x, ty_ = blockIdx.y;
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int x0 = (tile % nbx) * kTW, y0 = row0 + (tile / nbx) * kTH;
+    const int x0 = tx_ * kTW, y0 = row0 + ty_ * kTH;
     const int cq = lane & 31;
     const int xs = x0 + 4 * cq;                     // this lane's 4 columns
     const int r0 = 2 * wave + (lane >> 5);          // this lane's first tile row (then every 8th)
