@@ -291,10 +291,12 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
     __shared__ TileInfo s_info;
 
-    // Tile order: plain grid coordinates.  An XCD-aware remap (each XCD walking a contiguous run
-    // of tiles, WX_REMAP) measured no faster: a 128-px tile's gray2 / mask rows are whole 128-B
-    // lines, so neighbours share only the footprint margins, and the remap's divisions cost VALU.
-#ifdef WX_REMAP
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs; remap the linear id so
+    // each XCD walks a contiguous run of tiles (row-major).  Horizontally adjacent tiles share the
+    // 128-B lines at their footprints' margins: in one L2 they are fetched once (PMC: 529 MB read
+    // per 4K x32 launch = 1.0x the algorithmic bytes; plain grid order, tiles of a row spread over
+    // the XCDs: 803 MB).
+#ifndef WX_PLAIN_ORDER
     const int nbx = gridDim.x, nby = gridDim.y;
     int bid = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
     {
