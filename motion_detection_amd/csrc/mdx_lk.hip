@@ -414,6 +414,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER
     const long long T = (long long)batch * ngroups;
     const long long cb = T * xcd / 8, ce = T * (xcd + 1) / 8;     // this XCD's range of the work list
     const int p0 = (int)(cb / ngroups);
+    const uint32_t off0 = (uint32_t)(cb - (long long)p0 * ngroups);   // cb's group within pair p0
     const int np = ce > cb ? (int)((ce - 1) / ngroups) - p0 + 1 : 1;
     int* ctr = qctr + level * 8 + xcd;
     const ClassLevel& C = a.plan.lv[level];
@@ -466,9 +467,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER
                 if (cb + gi >= ce) {
                     dead = true;
                 } else {
-                    const long long gl = cb + gi;
-                    pair = (int)(gl / ngroups);
-                    q = group_geom<G, UW>(a, C, level, (int)(gl - (long long)pair * ngroups), sl);
+                    // position in the XCD's range relative to its first pair: 32-bit division
+                    const uint32_t r = off0 + (uint32_t)gi, dp = r / (uint32_t)ngroups;
+                    pair = p0 + (int)dp;
+                    q = group_geom<G, UW>(a, C, level, (int)(r - dp * (uint32_t)ngroups), sl);
                     q.ubase += (uint32_t)((long long)(pair - p0) * a.plan.bytes_per_pair);
                     jrel = (uint32_t)((long long)(pair - p0) * a.g.img_bytes);
                     pt = q.gx * a.ny + q.gy;
