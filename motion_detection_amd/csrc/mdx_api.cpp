@@ -28,7 +28,7 @@ struct mdx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;               // LK class / A kernels run ahead here (MDX_LK_AUX=0: off)
-    hipEvent_t lkev[kMaxLevels + 1] = {};
+    hipEvent_t lkev[kMaxLevels + 2] = {};    // launch_lk_v2's + the first frames' pyramids ready
     mdx_params prm{};
     int max_w = 0, max_h = 0, max_batch = 0;
     DevBuf pyr1, pyr2, der, fits;            // pyramid / derivative / fit workspace
@@ -318,7 +318,7 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     const char* ea = std::getenv("MDX_LK_AUX");
     if (!ea || std::atoi(ea) != 0) {
         bool ok = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;
-        for (int i = 0; ok && i <= kMaxLevels; i++)
+        for (int i = 0; ok && i <= kMaxLevels + 1; i++)
             ok = hipEventCreateWithFlags(&c->lkev[i], hipEventDisableTiming) == hipSuccess;
         if (!ok) {
             g_create_err = "aux stream / event creation failed";
@@ -442,7 +442,7 @@ static inline void mark(mdx_ctx* c, int i)
 // themselves; otherwise the single kernel, after the Scharr planes unless the caller already
 // computed them (have_scharr).  a: every field but the class-plan ones.
 static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, int h, int gy0, int gy1,
-                  bool have_scharr)
+                  bool have_scharr, hipEvent_t prev_ready = nullptr)
 {
     int rc;
     hipStream_t s = c->stream;
@@ -476,7 +476,7 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
     const size_t abytes = (size_t)g.nlev * batch * npts * sizeof(float4);
     if ((rc = ensure(c, c->Abuf, abytes + (size_t)batch * kMaxLevels * 8 * sizeof(int))) != MDX_OK) return rc;
     HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
-                                  reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes)));
+                                  reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes), prev_ready));
     return MDX_OK;
 }
 
@@ -512,7 +512,17 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
     mark(c, 0);
     HIP_OR_RETURN(c, launch_gray_pad(s, batch, d_img1, d_img2, w, h, stride, (long long)frame_stride, fmt, pyr1, pyr2, g));
     mark(c, 1);
-    for (int l = 1; l < g.nlev; l++) HIP_OR_RETURN(c, launch_pyrdown(s, batch, pyr1, pyr2, g, l));
+    // The class planes and A sums need only the first frames' pyramids: build those first and let
+    // the aux stream start on them while the second frames' pyramids are built
+    hipEvent_t prev_ready = nullptr;
+    if (c->aux && c->lk_impl == 2) {
+        for (int l = 1; l < g.nlev; l++) HIP_OR_RETURN(c, launch_pyrdown(s, batch, pyr1, pyr2, g, l, 1));
+        HIP_OR_RETURN(c, hipEventRecord(c->lkev[kMaxLevels + 1], s));
+        prev_ready = c->lkev[kMaxLevels + 1];
+        for (int l = 1; l < g.nlev; l++) HIP_OR_RETURN(c, launch_pyrdown(s, batch, pyr1, pyr2, g, l, 2));
+    } else {
+        for (int l = 1; l < g.nlev; l++) HIP_OR_RETURN(c, launch_pyrdown(s, batch, pyr1, pyr2, g, l));
+    }
     mark(c, 2);
     // Scharr derivatives feed only the LK.  The class-plane LK launches them itself, on its
     // aux stream right before each level's class planes, so they overlap the coarser levels'
@@ -535,7 +545,7 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         a.eps2 = e * e;
         a.next_pts = d_np;
         a.status = d_st;
-        if ((rc = run_lk(c, g, a, batch, w, h, gy0, gy1, false)) != MDX_OK) return rc;
+        if ((rc = run_lk(c, g, a, batch, w, h, gy0, gy1, false, prev_ready)) != MDX_OK) return rc;
     }
     mark(c, 4);
     if ((rc = ensure(c, c->csum, classify_scratch_bytes(batch, npts))) != MDX_OK) return rc;

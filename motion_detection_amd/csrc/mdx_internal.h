@@ -107,10 +107,12 @@ struct LkArgs {
 };
 
 // Launchers (mdx_kernels.hip).  All enqueue on `s`.
+// fsel: 0 both frames of every pair, 1 the first frame only, 2 the second frame only
 hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const uint8_t* in2, int w, int h,
                            int stride, long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2,
-                           const Geometry& g);
-hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level);
+                           const Geometry& g, int fsel = 0);
+hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level,
+                          int fsel = 0);
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level);
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
 // Trajectory subspace RANSAC (fitSubspace): mean-subtracted data, nhyp hypotheses of d columns
@@ -127,9 +129,11 @@ hipError_t launch_traj_update(hipStream_t s, int npts, const float* next_pts, co
                               double* vectors, float* start_pts, int* num);
 // Ab: [nlev][batch][npts] per-point (A11, A12, A22, 1/D); qctr: [batch][kMaxLevels][8] queue
 // heads.  aux (may be null): second stream for the flow-independent class / A kernels; ev: kMaxLevels
-// + 1 events (no timing) used to order the two streams.
+// + 1 events (no timing) used to order the two streams.  prev_ready (may be null): recorded by the
+// caller once the first frames' pyramids exist; the aux work waits on it instead of on everything
+// enqueued on s so far (the second frames' pyramids may still be in flight on s).
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
-                        float4* Ab, int* qctr);
+                        float4* Ab, int* qctr, hipEvent_t prev_ready = nullptr);
 // Grid rows [gy0, gy1) only (a row band; others are neither written nor counted).  cand != null:
 // row-band mode -- the band's count and first four accepted points go to *cand (one record per
 // pair) instead of a fit.

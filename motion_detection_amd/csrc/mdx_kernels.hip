@@ -88,9 +88,9 @@ __device__ __forceinline__ void gray_chunk(const uint8_t* s, int px0, int w, int
 __global__ __launch_bounds__(256) void k_gray_pad(const uint8_t* __restrict__ in1, const uint8_t* __restrict__ in2,
                                                   int w, int h, int stride, long long frame_stride, int fmt,
                                                   uint8_t* __restrict__ pyr1, uint8_t* __restrict__ pyr2,
-                                                  long long img_bytes, Level L, int nchunk)
+                                                  long long img_bytes, Level L, int nchunk, int fsel)
 {
-    const int which = blockIdx.z & 1, pair = blockIdx.z >> 1;
+    const int which = fsel ? fsel - 1 : blockIdx.z & 1, pair = fsel ? blockIdx.z : blockIdx.z >> 1;
     const int c = 2 * (blockIdx.x * blockDim.x + threadIdx.x) + 1;   // chunk 0 is all margin
     const int py = blockIdx.y - kPad;
     if (c > nchunk) return;
@@ -127,10 +127,10 @@ __device__ __forceinline__ uint32_t pyr_px(const uint8_t* src, int sp, int cx, i
 }
 
 __global__ __launch_bounds__(256) void k_pyrdown(uint8_t* __restrict__ pyr1, uint8_t* __restrict__ pyr2,
-                                                 long long img_bytes, Level S, Level D, int nchunk)
+                                                 long long img_bytes, Level S, Level D, int nchunk, int fsel)
 {
     // 4 destination pixels (one dword) per thread
-    const int which = blockIdx.z & 1, pair = blockIdx.z >> 1;
+    const int which = fsel ? fsel - 1 : blockIdx.z & 1, pair = fsel ? blockIdx.z : blockIdx.z >> 1;
     const int c = blockIdx.x * blockDim.x + threadIdx.x + 6;         // dword chunks 0..5 are margin
     const int py = blockIdx.y - kPad;
     if (c > nchunk) return;
@@ -888,21 +888,21 @@ __global__ void k_export_fit(const PairFit* __restrict__ fits, int batch, double
 static inline int last_chunk16(int w) { return (kXOff + w + kPad - 1) / 16; }
 
 hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const uint8_t* in2, int w, int h, int stride,
-                           long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g)
+                           long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int fsel)
 {
     const int nchunk = last_chunk16(w);
-    const dim3 grid((nchunk + 127) / 128, h + 2 * kPad, 2 * batch);   // two chunks per thread
+    const dim3 grid((nchunk + 127) / 128, h + 2 * kPad, fsel ? batch : 2 * batch);   // two chunks per thread
     hipLaunchKernelGGL(k_gray_pad, grid, dim3(64), 0, s, in1, in2, w, h, stride, frame_stride, fmt, pyr1, pyr2,
-                       g.img_bytes, g.lv[0], nchunk);
+                       g.img_bytes, g.lv[0], nchunk, fsel);
     return hipGetLastError();
 }
 
-hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level)
+hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level, int fsel)
 {
     const Level& D = g.lv[level];
     const int nchunk = (kXOff + D.w + kPad - 1) / 4;                 // last dword chunk
-    const dim3 grid((nchunk - 6 + 1 + 63) / 64, D.h + 2 * kPad, 2 * batch);
-    hipLaunchKernelGGL(k_pyrdown, grid, dim3(64), 0, s, pyr1, pyr2, g.img_bytes, g.lv[level - 1], D, nchunk);
+    const dim3 grid((nchunk - 6 + 1 + 63) / 64, D.h + 2 * kPad, fsel ? batch : 2 * batch);
+    hipLaunchKernelGGL(k_pyrdown, grid, dim3(64), 0, s, pyr1, pyr2, g.img_bytes, g.lv[level - 1], D, nchunk, fsel);
     return hipGetLastError();
 }
 

@@ -705,7 +705,7 @@ static void launch_iter(hipStream_t s, int batch, const LkArgs& a, const uint8_t
 }
 
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
-                        float4* Ab, int* qctr)
+                        float4* Ab, int* qctr, hipEvent_t prev_ready)
 {
     // An XCD range spans at most ceil(n/8) + 1 pairs; its class slabs (and pyramids) must stay
     // addressable by 32-bit buffer offsets, so very large batches of large frames run in
@@ -731,8 +731,12 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         uint8_t* bcls = cls + (long long)p * a.plan.bytes_per_pair;
         int* bq = qctr + si * kMaxLevels * 8;
         if (aux) {
-            if (hipError_t e = hipEventRecord(ev[kMaxLevels], s)) return e;
-            if (hipError_t e = hipStreamWaitEvent(sa, ev[kMaxLevels], 0)) return e;
+            hipEvent_t ready = prev_ready;
+            if (!ready || p) {   // later sub-batches follow everything on s (their slabs are reused)
+                if (hipError_t e = hipEventRecord(ev[kMaxLevels], s)) return e;
+                ready = ev[kMaxLevels];
+            }
+            if (hipError_t e = hipStreamWaitEvent(sa, ready, 0)) return e;
         }
         for (int l = a.maxl; l >= 0; l--) {
             const ClassLevel& C = a.plan.lv[l];
