@@ -119,7 +119,7 @@ __device__ __forceinline__ void wave_lds_fence()
 #endif
 
 #ifndef LKX_WPE_ITER
-#define LKX_WPE_ITER 6   // k_lk_iter: 6 waves/SIMD (<= 80 VGPRs; 6 KiB LDS each fits 24 per CU)
+#define LKX_WPE_ITER 5   // k_lk_iter: 5 waves/SIMD (<= 102 VGPRs; measured 3% faster than 6 at <= 80)
 #endif
 typedef __attribute__((address_space(3))) void* lds_ptr;
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
