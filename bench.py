@@ -108,6 +108,20 @@ def make_batch(w: int, h: int, batch: int, unique: int, seed0: int, threads: int
     return g1, g2, Ht, uniq
 
 
+def host_cores() -> dict:
+    """What this host offers: nproc (the CPUs this process may run on) and the cgroup CPU quota,
+    which on a shared GPU box can be far smaller than nproc."""
+    nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": nproc, "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline(uniq, w, h, seconds: float, threads: int):
     """The C oracle on this host: whole reference path per pair, `threads` threads over LK
     points / warp rows (like OpenCV's parallel_for_).  Bounded sample: pairs are processed
@@ -123,20 +137,71 @@ def cpu_baseline(uniq, w, h, seconds: float, threads: int):
         if el >= seconds:
             break
     return dict(value=round(n * w * h / 1e6 / el, 3), unit="Mpixels/s", cores=threads, kind="port",
-                sample=f"{n} x {w}x{h} gray pairs, full reference path (oracle/mdx_oracle.c, {threads} threads), "
-                       f"{el:.1f} s wall")
+                sample=f"{n} x {w}x{h} gray pairs, full reference path (oracle/mdx_oracle.c, scalar C restatement of "
+                       f"the OpenCV 2.4 path, {threads} thread(s) over LK points / warp rows), {el:.1f} s wall")
+
+
+REHEARSE = False   # --rehearse: ranks beyond the visible devices may share device 0
 
 
 def open_ctx(D: Dist, w: int, h: int, batch: int, **params):
-    """One context on this rank's GPU.  Ranks beyond the visible devices share them round-robin
-    (rehearsing a multi-rank run on a one-GPU box)."""
+    """One context on this rank's GPU (LOCAL_RANK).  A rank whose device is not visible is an
+    error (exit 3) unless --rehearse is given: then it shares device 0, and the JSON line's n_gpus
+    counts the distinct devices actually used, never the ranks."""
     try:
         return mdx.Context(D.local_rank, w, h, batch, **params)
     except mdx.MdxError as e:
-        if "out of range" not in str(e):
+        if "out of range" not in str(e) and "invalid device" not in str(e).lower():
             raise
-        log(f"rank {D.rank}: device {D.local_rank} not visible, sharing device 0")
+        if not REHEARSE:
+            log(f"rank {D.rank}: device {D.local_rank} is not visible ({e}); refusing to share a GPU "
+                f"(pass --rehearse to rehearse {D.world} ranks on fewer devices)")
+            sys.exit(3)
+        log(f"rank {D.rank}: device {D.local_rank} not visible, sharing device 0 (--rehearse)")
         return mdx.Context(0, w, h, batch, **params)
+
+
+def device_summary(records):
+    """records: one (rank, device, pci_bus_id) per rank.  Returns the JSON fields describing the
+    devices used: n_gpus = number of DISTINCT physical devices (PCI ids), not ranks."""
+    recs = sorted(records)
+    pcis = [r[2] for r in recs]
+    return {"n_gpus": len(set(pcis)), "ranks": len(recs),
+            "devices": [{"rank": r[0], "device": r[1], "pci": r[2]} for r in recs]}
+
+
+def gather_devices(D: Dist, ctx) -> dict:
+    """Every rank's (rank, device id, PCI bus id), gathered over the host group."""
+    rec = json.dumps([D.rank, ctx.device, ctx.device_pci()]).encode().ljust(128)
+    parts = D.allgather_bytes(rec)
+    return device_summary([tuple(json.loads(p.decode().strip())) for p in parts])
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N fresh worker processes of this script (one
+    per GPU, RANK = LOCAL_RANK = i, WORLD_SIZE = N, gloo rendezvous on 127.0.0.1) and return the
+    worst exit code.  The parent never touches the GPU and is never replaced (no exec)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs) if any(rcs) else 0
+
+
+def probe_ranks(D: Dist) -> None:
+    """--probe-ranks: the launch plumbing alone (no GPU): every rank reports its env over gloo."""
+    rec = json.dumps([D.rank, D.local_rank, D.world, os.getpid()]).encode().ljust(128)
+    parts = [json.loads(p.decode().strip()) for p in D.allgather_bytes(rec)]
+    if D.rank == 0:
+        print(json.dumps({"probe": sorted(parts)}), flush=True)
+    D.close()
 
 
 def main_c4(args, D: Dist, threads: int):
@@ -153,6 +218,7 @@ def main_c4(args, D: Dist, threads: int):
     per_rank = -(-K // D.world)
     a, b, _ = mdx.synth_pair(SEED0 + 4, w, h, 3, threads)       # every rank: the same frame pair
     ctx = open_ctx(D, w, h, 1, pixel_step=ps, min_vector_size=1.0)
+    devs = gather_devices(D, ctx)
     n = mdx.grid_count(w, h, ps)
     d = {k: ctx.dev_alloc(sz) for k, sz in dict(i1=a.nbytes, i2=b.nbytes, np=n * 8, st=n, cand=per_rank * 96,
                                                cands=K * 96, mask=w * h, num=4).items()}
@@ -220,7 +286,9 @@ def main_c4(args, D: Dist, threads: int):
         "metric": METRIC,
         "value": round(args.steps * w * h / el_max / 1e6, 2),
         "unit": "Mpixels/s",
-        "n_gpus": D.world,
+        "n_gpus": devs["n_gpus"],
+        "ranks": devs["ranks"],
+        "devices": devs["devices"],
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(el_max / args.steps * 1e3, 3),
@@ -300,7 +368,7 @@ def main():
     ap.add_argument("--roofline-batch", type=int, default=32)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--only-roofline", action="store_true", help="profiling aid: only the warp+diff roofline leg")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="per CPU-baseline leg (nproc threads, 1 thread)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_warp_diff.json"),
                     help="per-launch HBM traffic measured by rocprofv3 --pmc (scripts/profile.sh)")
@@ -309,11 +377,21 @@ def main():
     ap.add_argument("--bands", type=int, default=0, help="c4: row bands (default: one per rank)")
     ap.add_argument("--no-live", action="store_true", help="skip the node's live trajectory + RANSAC leg")
     ap.add_argument("--no-4k", action="store_true", help="skip the whole-path 4K leg (config C2)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="allow more ranks than visible GPUs (they share device 0; n_gpus counts distinct devices)")
+    ap.add_argument("--probe-ranks", action="store_true", help="launch plumbing only: ranks report over gloo, no GPU")
     args = ap.parse_args()
+    global REHEARSE
+    REHEARSE = args.rehearse
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))          # one fresh worker process per GPU
     D = Dist()
     if args.gpus != D.world:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {D.world}; using WORLD_SIZE")
+    if args.probe_ranks:
+        return probe_ranks(D)
+    # host threads for the synthetic generator (bounded: the GPU box's CPU share is 16)
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
     if args.workload == "c4":
         return main_c4(args, D, threads)
@@ -327,6 +405,7 @@ def main():
     if args.only_roofline:
         B, unique = 1, 1
     ctx = open_ctx(D, w, h, B, pixel_step=ps, min_vector_size=1.0)
+    devs = gather_devices(D, ctx)
     d1, d2 = ctx.dev_alloc(g1.nbytes), ctx.dev_alloc(g2.nbytes)
     dmask = ctx.dev_alloc(B * w * h)
     dnum = ctx.dev_alloc(B * 4)
@@ -430,9 +509,12 @@ def main():
         rctx.close()
         del r1, r2
 
-    cpu = None
+    cpu = cpu1 = None
     if D.world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(uniq, w, h, args.cpu_seconds, threads)
+        hc = host_cores()
+        cpu = cpu_baseline(uniq, w, h, args.cpu_seconds, hc["nproc"])   # all host cores (nproc), stated
+        cpu.update(hc)
+        cpu1 = cpu_baseline(uniq, w, h, args.cpu_seconds, 1)             # one core
     live = None
     if D.world == 1 and not args.no_live and not args.only_roofline:
         live = live_leg(D.local_rank, w, h, threads, with_cpu=not args.no_cpu)
@@ -442,7 +524,7 @@ def main():
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "Mpixels/s",
-        "n_gpus": D.world,
+        "n_gpus": devs["n_gpus"],
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(el_max / full_steps * 1e3, 3),
@@ -458,6 +540,10 @@ def main():
                    "parallelism": f"{D.world} independent stream shard(s), one per GPU, no collectives"},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "cpu_baseline_1core": cpu1,
+        "ranks": devs["ranks"],
+        "devices": devs["devices"],
+        "build": mdx._lib.build_info(),
         "stage_ms_per_step": stages,
         "dominant_kernel": {"name": "k_lk", "share_of_step": round(lk_share, 4) if lk_share else None,
                             "bound": "valu/lds (exact-order float chains), not hbm",

@@ -80,6 +80,12 @@ int mdx_get_params(const mdx_ctx* ctx, mdx_params* p);
 /* The context's HIP stream (hipStream_t as void*) and device id; for interop only. */
 void* mdx_stream(mdx_ctx* ctx);
 int mdx_device(const mdx_ctx* ctx);
+/* PCI bus id ("0000:xx:yy.z") of the context's device, so multi-GPU records can show which
+ * distinct devices the ranks ran on. */
+int mdx_device_pci(const mdx_ctx* ctx, char* buf, int len);
+/* Build provenance: "src_sha256=<sha256 of the library's sources> arch=gfx950", compiled in by
+ * csrc/Makefile.  tests/test_abi.py checks it against the sources in the tree. */
+const char* mdx_build_info(void);
 int mdx_sync(mdx_ctx* ctx);
 /* hipDeviceSynchronize on the context's device (all streams). */
 int mdx_device_sync(mdx_ctx* ctx);

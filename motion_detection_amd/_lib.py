@@ -34,8 +34,12 @@ EXPORTED = [
     "mdx_flow_warp_diff", "mdx_flow_warp_diff_batch_dev", "mdx_warp_diff_dev", "mdx_dev_alloc",
     "mdx_dev_free", "mdx_memcpy_h2d", "mdx_memcpy_d2h", "mdx_enable_timing", "mdx_timing_calls", "mdx_stage_ms",
     "mdx_synth_pair", "mdx_debug_copy", "mdx_band_flow_dev", "mdx_band_fit_warp_dev", "mdx_flow_trajectory",
-    "mdx_srand", "mdx_rand", "mdx_fit_subspace",
+    "mdx_srand", "mdx_rand", "mdx_fit_subspace", "mdx_device_pci", "mdx_build_info",
 ]
+
+# csrc/Makefile STAMPED: the files whose bytes the library's provenance stamp hashes, in order
+STAMPED = ["Makefile", "mdx_internal.h", "mdx_api.cpp", "mdx_kernels.hip", "mdx_lk.hip", "mdx_warp.hip",
+           "mdx_subspace.hip", "synth.cpp", os.path.join("..", "..", "include", "mdx.h")]
 
 
 class MdxBandCand(C.Structure):
@@ -63,11 +67,30 @@ class MdxError(RuntimeError):
     """Raised for every negative return code of the C-ABI."""
 
 
-def build(force: bool = False) -> str:
-    """Compile libmdx.so for gfx950 with hipcc (csrc/Makefile)."""
+def build(force: bool = True) -> str:
+    """Compile libmdx.so for gfx950 with hipcc (csrc/Makefile); force (default) rebuilds every
+    object from the sources in the tree (make -B)."""
     cmd = ["make", "-s", "-C", CSRC] + (["-B"] if force else [])
     subprocess.run(cmd, check=True)
     return LIB_PATH
+
+
+def source_sha256() -> str:
+    """sha256 of the library's sources as csrc/Makefile stamps them into mdx_build_info()."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in STAMPED:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def build_info() -> dict:
+    """The loaded library's provenance stamp, and whether it matches the sources in this tree."""
+    raw = lib().mdx_build_info().decode()
+    kv = dict(part.split("=", 1) for part in raw.split())
+    kv["matches_tree"] = kv.get("src_sha256") == source_sha256()
+    return kv
 
 
 _lib = None
@@ -104,6 +127,10 @@ def lib() -> C.CDLL:
     L.mdx_device.restype = C.c_int
     L.mdx_sync.argtypes = [vp]
     L.mdx_sync.restype = C.c_int
+    L.mdx_device_pci.argtypes = [vp, C.c_char_p, C.c_int]
+    L.mdx_device_pci.restype = C.c_int
+    L.mdx_build_info.argtypes = []
+    L.mdx_build_info.restype = C.c_char_p
     L.mdx_device_sync.argtypes = [vp]
     L.mdx_device_sync.restype = C.c_int
     L.mdx_flow_warp_diff.argtypes = [vp, u8p, u8p, C.c_int, C.c_int, C.c_int, C.c_int, f32p, u8p, f64p, u8p,

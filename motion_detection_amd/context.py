@@ -93,6 +93,16 @@ class Context:
         except Exception:
             pass
 
+    @property
+    def device(self) -> int:
+        return lib().mdx_device(self._h)
+
+    def device_pci(self) -> str:
+        """PCI bus id of the context's device (distinct per physical GPU)."""
+        buf = C.create_string_buffer(64)
+        self._check(lib().mdx_device_pci(self._h, buf, 64))
+        return buf.value.decode()
+
     def _check(self, rc: int) -> int:
         if rc < 0:
             raise MdxError(f"mdx error {rc}: {lib().mdx_last_error(self._h).decode()}")

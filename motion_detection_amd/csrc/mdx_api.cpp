@@ -360,6 +360,11 @@ extern "C" int mdx_destroy(mdx_ctx* c)
 extern "C" const char* mdx_last_error(const mdx_ctx* c) { return c ? c->err.c_str() : "null context"; }
 extern "C" void* mdx_stream(mdx_ctx* c) { return c ? (void*)c->stream : nullptr; }
 extern "C" int mdx_device(const mdx_ctx* c) { return c ? c->device : -1; }
+extern "C" int mdx_device_pci(const mdx_ctx* c, char* buf, int len)
+{
+    if (!c || !buf || len < 16) return MDX_EINVAL;
+    return hipDeviceGetPCIBusId(buf, len, c->device) == hipSuccess ? MDX_OK : MDX_EHIP;
+}
 
 extern "C" int mdx_set_params(mdx_ctx* c, const mdx_params* p)
 {

@@ -137,3 +137,15 @@ def test_golden_manifest_covers_fixtures():
     man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))
     for name in man:
         assert os.path.exists(os.path.join(ROOT, "tests", "golden", name + ".npz"))
+
+
+def test_library_built_from_the_tree_sources(mdx):
+    """Provenance: the loaded libmdx.so carries the sha256 of the sources it was compiled from
+    (csrc/Makefile stamps it); it must equal the hash of the sources in this tree, so a stale or
+    foreign library cannot pass the GPU tests."""
+    from motion_detection_amd import _lib
+    if os.environ.get("MDX_LIB_PATH"):
+        pytest.skip("variant library selected by MDX_LIB_PATH")
+    info = _lib.build_info()
+    assert info["arch"] == "gfx950"
+    assert info["matches_tree"], (info, _lib.source_sha256())

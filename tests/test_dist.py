@@ -68,3 +68,41 @@ def test_single_rank_needs_no_torch():
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     out = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True, timeout=120)
     assert out.stdout.split() == ["True", "False"], out.stdout + out.stderr
+
+
+def _bench_env():
+    return {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                                                             "MASTER_ADDR", "MASTER_PORT")}
+
+
+def test_gpus_n_spawns_n_ranks_without_a_launcher():
+    """`python bench.py --gpus 2` (no torchrun) starts two fresh worker processes with RANK /
+    LOCAL_RANK / WORLD_SIZE set, which meet over gloo on 127.0.0.1."""
+    import json
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--probe-ranks"], env=_bench_env(), cwd=ROOT,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1                                # rank 0 prints the one line
+    probe = json.loads(lines[0])["probe"]
+    assert [p[:3] for p in probe] == [[0, 0, 2], [1, 1, 2]]
+    assert probe[0][3] != probe[1][3]                     # two distinct processes
+
+
+def test_gpus_n_without_devices_fails_instead_of_sharing():
+    """No silent device sharing: ranks whose GPU is not visible end the run with a non-zero exit
+    and no JSON line (here: no GPU at all)."""
+    env = dict(_bench_env(), HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu"],
+                         env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert out.returncode != 0
+    assert not [l for l in out.stdout.splitlines() if l.startswith("{")]
+
+
+def test_device_summary_counts_distinct_devices():
+    import bench
+    two = bench.device_summary([(1, 1, "0000:15:00.0"), (0, 0, "0000:05:00.0")])
+    assert two["n_gpus"] == 2 and two["ranks"] == 2
+    assert [d["rank"] for d in two["devices"]] == [0, 1]
+    shared = bench.device_summary([(0, 0, "0000:05:00.0"), (1, 0, "0000:05:00.0")])   # --rehearse on one GPU
+    assert shared["n_gpus"] == 1 and shared["ranks"] == 2
