@@ -52,15 +52,9 @@ typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
 
 constexpr int kTW = 128;     // tile width: two reference block columns (bw0 = 64)
 constexpr int kBW = 64;      // reference block width of the fast path
-#ifndef WX_TH
-#define WX_TH 64
-#endif
-constexpr int kTH = WX_TH;   // tile rows
+constexpr int kTH = 64;      // tile rows
 constexpr int kSP = 256;     // staged row pitch: tap address = (row << 8) | col, one v_perm
-#ifndef WX_SH
-#define WX_SH (WX_TH + 12)
-#endif
-constexpr int kSH = WX_SH;   // staged rows (tile height + scale/rotation margin)
+constexpr int kSH = kTH + 12;   // staged rows (tile height + scale/rotation margin)
 
 __device__ __forceinline__ int clamp_int_from_double(double v)
 {
@@ -202,18 +196,11 @@ __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t sr
         uint32_t ad[4], wys[4], wxs[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-#ifdef WX_DIRECT
-            // weights computed: (32 - fy, fy) and 64 * (32 - fx, fx)
-            ad[k] = src_base + ((ys_[k] >> 5) << 8 | (xs_[k] >> 5));
-            wys[k] = (ys_[k] & 31u) * 65535u + 32u;
-            wxs[k] = (xs_[k] & 31u) * (64u * 65535u) + 2048u;
-#else
             // 8X: byte 1 is the staged column (row), bits 3..7 index the 8-B weight table
             const uint32_t lx = xs_[k] << 3, ly = ys_[k] << 3;
             ad[k] = src_base + __builtin_amdgcn_perm(ly, lx, 0x0c0c0501u);   // (row << 8) | col
             wys[k] = *(lds_u32*)(tab8 + (ly & 0xf8u));       // (32 - fy, fy)
             wxs[k] = *(lds_u32*)(tab8 + (lx & 0xf8u) + 4);   // 64 * (32 - fx, fx)
-#endif
         }
         // taps: four byte reads per pixel, c0 = (v00, v01), c1 = (v10, v11) as u16 halves.
         // (ds_read_*_d16_hi does not preserve the low half on gfx950 with SRAM ECC, and unaligned
@@ -226,9 +213,6 @@ __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t sr
             c1s[k] = (uint32_t)p[kSP] | ((uint32_t)p[kSP + 1] << 16);
         }
         uint32_t e[4];
-#ifdef WX_DEBUG_VAL
-        uint32_t sv_[4];
-#endif
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const u16x2v c0 = __builtin_bit_cast(u16x2v, c0s[k]), c1 = __builtin_bit_cast(u16x2v, c1s[k]);
@@ -237,17 +221,9 @@ __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t sr
             const uint32_t s = __builtin_amdgcn_udot2(q, __builtin_bit_cast(u16x2v, wxs[k]), 32u, false);
             const uint32_t g16 = __builtin_amdgcn_perm(0u, G[i], 0x0c000c0cu | ((uint32_t)k << 16));   // g_k << 16
             asm("v_sad_u32 %0, %1, %2, %3" : "=v"(e[k]) : "v"(s), "v"(g16), "s"(bias));   // bit 31: moving
-#ifdef WX_DEBUG_VAL
-            sv_[k] = s;
-#endif
         }
         // v_perm selectors 9 / 11 replicate bit 31 of src1 / src0: 0xff or 0x00 bytes
-#ifndef WX_DEBUG_VAL
         const uint32_t out = __builtin_amdgcn_perm(e[1], e[0], 0x0c0c0b09u) | __builtin_amdgcn_perm(e[3], e[2], 0x0b090c0cu);
-#else   // debug build: the warped values instead of the mask
-        uint32_t out = 0;
-        for (int k = 0; k < 4; k++) out |= ((sv_[k] + 32736u) >> 16) << (8 * k);
-#endif
         __builtin_amdgcn_raw_buffer_store_b32(out, mrs, (int)moff, i * ms, 0);
     }
 }
@@ -296,7 +272,6 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     // 128-B lines at their footprints' margins: in one L2 they are fetched once (PMC: 529 MB read
     // per 4K x32 launch = 1.0x the algorithmic bytes; plain grid order, tiles of a row spread over
     // the XCDs: 803 MB).
-#ifndef WX_PLAIN_ORDER
     const int nbx = gridDim.x, nby = gridDim.y;
     int bid = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
     {
@@ -305,9 +280,6 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     }
     const int pair = bid / (nbx * nby), tile = bid - pair * (nbx * nby);
     const int tx_ = tile % nbx, ty_ = tile / nbx;
-#else
-    const int pair = blockIdx.z, tx_ = blockIdx.x, ty_ = blockIdx.y;
-#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int x0 = tx_ * kTW, y0 = row0 + ty_ * kTH;
     const int cq = lane & 31;
@@ -376,11 +348,7 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
                 uint32_t off = (uint32_t)((t.sya + ro) * g1_pitch + sx);
                 const uint32_t step = (uint32_t)(rpp * g1_pitch);
                 for (int r = ro; r < t.sh; r += rpp, off += step) {
-#ifdef WX_NO_STAGE   // WX_*: timing-only builds (scripts/warp_variants.sh), results invalid
-                    const v4u v = {(uint32_t)r, (uint32_t)sx, off, (uint32_t)ch};
-#else
                     const v4u v = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)off, 0, 0);
-#endif
                     *reinterpret_cast<uint4*>(&s_src[r * kSP + 16 * ch]) = make_uint4(v.x, v.y, v.z, v.w);
                 }
             } else {

@@ -1,0 +1,845 @@
+// mdx_warp.hip -- rows A8-A10 fused: warpPerspective(gray1, M) + absdiff(., gray2) +
+// threshold(., 190, 255, BINARY) (reference common/src/optical_flow_calculator.cpp:124-127),
+// bit-exact to OpenCV 2.4's imgwarp.cpp WarpPerspectiveInvoker + remapBilinear<FixedPtCast> with
+// BORDER_CONSTANT 0.
+//
+// Reference arithmetic per destination pixel (x, y), M = inverse of the fitted H:
+//   blocks of bw0 x bh0 (bh0 = min(16, H), bw0 = min(1024 / bh0, W)); xb = bw0 * floor(x / bw0)
+//   X0 = M0*xb + M1*y + M2,  W0 = M6*xb + M7*y + M8           (FP64, this evaluation order)
+//   W  = W0 + M6*x1, Wd = W ? 32/W : 0,  x1 = x - xb
+//   X  = cvRound(clamp((X0 + M0*x1) * Wd)),  Y likewise        (1/32-pixel fixed point)
+//   sx = X >> 5, fx = X & 31, ...;  out = (sum v_i * w_i + 2^14) >> 15 with w_i from (fx, fy)
+//   mask = |out - gray2| > thresh ? 255 : 0
+//
+// Fast path (affine M, bw0 == 64, dword-aligned buffers, the tile's source footprint small): one
+// 256-thread workgroup per 128 x 64 destination tile (two reference block columns; 64 rows
+// measured best: 32 doubles the per-tile setup, 128 halves the workgroups a CU holds).  Lane l of
+// wave w owns the 4 columns x0 + 4*(l & 31) .. +3 of rows y0 + 8i + 2w + (l >> 5), i = 0..7: a
+// half-wave is one tile row, so gray2 loads / mask stores are dwords, 128 contiguous bytes.
+//   * Footprint: X, Y are monotone in x and y inside a reference block for affine M, so the eight
+//     block corners bound the tile's taps exactly.  It is staged once into LDS as raw bytes
+//     (16-B loads, ds_write_b128), zero outside the image (= BORDER_CONSTANT 0 per tap), at a row
+//     pitch of 256 B.
+//   * Coordinates, per pixel: one FP64 add (per-row X0 from an LDS table + per-column M0*x1 in
+//     registers) and one FMA with the magic constant 1.5*2^52 - 32*origin per axis, whose low word
+//     is cvRound(32*(...)) - 32*origin (round-half-even, exact for |X| < 2^30, checked per tile).
+//     When 32/M8 is not a power of two the product (...)*Wd is rounded first, as the reference
+//     does, and the add only rounds it to an integer.
+//   * Shifted left by 3, byte 1 of each low word is the staged source column (row) and bits 3..7
+//     are 8*fx (8*fy): the tap address (row << 8 | col) is ONE v_perm, and 8*f indexes a 32-entry
+//     LDS weight table (entry f: wy = (32-f, f), wx = 64*(32-f, f)).
+//   * Taps: four byte reads per pixel, c0 = (v00, v01), c1 = (v10, v11) as u16 halves.  Vertical
+//     with two packed u16 ops (op_sel splats the weight halves), q = c0*(32-fy) + c1*fy =
+//     (q0, q1) <= 8160; horizontal with one v_dot2_u32_u16: s = 64*(q0 (32-fx) + q1 fx) + 32.
+//   * Threshold without the >> 10: out = (S + 512) >> 10 with S = (s - 32)/64, and
+//     |out - g| > t  <=>  |s - 65536 g| >= 65536 t + 32800 (exact).
+//     v_sad_u32(s, g << 16, 2^31 - 65536 t - 32800) sets bit 31 iff the pixel moves (g << 16 is
+//     one v_perm of the gray2 dword); v_perm's sign-replicating selectors turn the four flags
+//     into the four 0x00/0xff mask bytes.
+//   * gray2 loads / mask stores go through buffer descriptors: lanes past the right edge get an
+//     out-of-range offset and rows past the band fall outside the mask descriptor, so the row
+//     loop is branch-free.  ~17 VALU per pixel (4 of them FP64), vs ~23 for the 64x128-tile
+//     design before it (rocprofv3 SQ_INSTS_VALU).
+// Everything else (perspective M, small frames, huge or far-away footprints) takes the general
+// per-pixel path, exact for any input.
+#include "mdx_internal.h"
+
+#include <limits.h>
+#include <stdlib.h>
+
+#include <type_traits>
+
+namespace mdx {
+
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+
+constexpr int kTW = 128;     // tile width: two reference block columns (bw0 = 64)
+constexpr int kBW = 64;      // reference block width of the fast path
+constexpr int kTH = 64;      // tile rows
+constexpr int kSP = 256;     // staged row pitch: tap address = (row << 8) | col, one v_perm
+constexpr int kSH = kTH + 12;   // staged rows (tile height + scale/rotation margin)
+
+__device__ __forceinline__ int clamp_int_from_double(double v)
+{
+    // std::max((double)INT_MIN, std::min((double)INT_MAX, v)) then cvRound
+    double r = (v < (double)INT_MAX) ? v : (double)INT_MAX;
+    r = ((double)INT_MIN < r) ? r : (double)INT_MIN;
+    return (int)__builtin_rint(r);
+}
+
+// General path: one destination pixel, any M, reading gray1 straight from global memory.
+__device__ __forceinline__ uint8_t warp_px_general(const double* M, const uint8_t* src, int pitch, int w, int h, int x,
+                                                   int y, int bw0, int g2v, int thresh)
+{
+    const int xb = (x / bw0) * bw0, x1 = x - xb;
+    const double X0 = M[0] * xb + M[1] * y + M[2];
+    const double Y0 = M[3] * xb + M[4] * y + M[5];
+    const double W0 = M[6] * xb + M[7] * y + M[8];
+    const double Wv = W0 + M[6] * x1;
+    const double Wd = Wv != 0.0 ? 32.0 / Wv : 0.0;
+    const int X = clamp_int_from_double((X0 + M[0] * x1) * Wd);
+    const int Y = clamp_int_from_double((Y0 + M[3] * x1) * Wd);
+    const int sx = min(max(X >> 5, -32768), 32767), sy = min(max(Y >> 5, -32768), 32767);
+    const int fx = X & 31, fy = Y & 31;
+    // (0,0) cell of BilinearTab_i is {32767,0,0,1}; for 8-bit data it yields the same value as
+    // {32768,0,0,0}, which is what the plain formula computes.
+    const int wt0 = (32 - fx) * (32 - fy) * 32, wt1 = fx * (32 - fy) * 32;
+    const int wt2 = (32 - fx) * fy * 32, wt3 = fx * fy * 32;
+    const bool ix0 = (unsigned)sx < (unsigned)w, ix1 = (unsigned)(sx + 1) < (unsigned)w;
+    const bool iy0 = (unsigned)sy < (unsigned)h, iy1 = (unsigned)(sy + 1) < (unsigned)h;
+    const int cx0 = min(max(sx, 0), w - 1), cx1 = min(max(sx + 1, 0), w - 1);
+    const int cy0 = min(max(sy, 0), h - 1), cy1 = min(max(sy + 1, 0), h - 1);
+    const uint8_t* ra = src + (long long)cy0 * pitch;
+    const uint8_t* rb = src + (long long)cy1 * pitch;
+    const int v0 = (ix0 && iy0) ? ra[cx0] : 0;
+    const int v1 = (ix1 && iy0) ? ra[cx1] : 0;
+    const int v2 = (ix0 && iy1) ? rb[cx0] : 0;
+    const int v3 = (ix1 && iy1) ? rb[cx1] : 0;
+    int v = (v0 * wt0 + v1 * wt1 + v2 * wt2 + v3 * wt3 + (1 << 14)) >> 15;
+    v = min(max(v, 0), 255);
+    return abs(v - g2v) > thresh ? 255 : 0;
+}
+
+struct TileInfo {
+    double wd;         // 32 / M8 (affine: W = M8 everywhere), 0 when M8 == 0
+    int fast;          // 1: fast path usable for this tile
+    int sxa, sya;      // staged origin (sxa multiple of 16)
+    int sw, sh;        // staged width (bytes), height (rows)
+};
+
+// Bounds of the tile's taps, from the reference arithmetic at the corners of its (one or two)
+// reference blocks, one corner per lane 0..7; fast = every |X|, |Y| < 2^30 (no clamp, magic
+// rounding exact) and the footprint fits the staging buffer.
+__device__ TileInfo tile_info(const double* M, int x0, int y0, int w, int yend, int lane)
+{
+    const double Wd = M[8] != 0.0 ? 32.0 / M[8] : 0.0;
+    const int nb = (x0 + kBW < w) ? 2 : 1;                       // reference blocks in the tile
+    const int b = ((lane >> 2) & 1) < nb ? ((lane >> 2) & 1) : 0;
+    const int xb = x0 + kBW * b;
+    const int cxl = min(kBW - 1, w - 1 - xb), cyl = min(kTH - 1, yend - 1 - y0);
+    const int c = lane & 3;
+    const int x1 = (c & 1) ? cxl : 0, y = y0 + ((c & 2) ? cyl : 0);
+    const double X0 = M[0] * xb + M[1] * y + M[2];
+    const double Y0 = M[3] * xb + M[4] * y + M[5];
+    const double px = (X0 + M[0] * x1) * Wd, py = (Y0 + M[3] * x1) * Wd;
+    const double lim = 1073741824.0;   // 2^30
+    int ok = (px > -lim && px < lim && py > -lim && py < lim) ? 1 : 0;
+    int sx = 0, sy = 0;
+    if (ok) {
+        sx = ((int)__builtin_rint(px)) >> 5;
+        sy = ((int)__builtin_rint(py)) >> 5;
+    }
+    int sx_lo = sx, sx_hi = sx, sy_lo = sy, sy_hi = sy;
+#pragma unroll
+    for (int m = 1; m <= 4; m <<= 1) {
+        sx_lo = min(sx_lo, __shfl_xor(sx_lo, m, 8));
+        sx_hi = max(sx_hi, __shfl_xor(sx_hi, m, 8));
+        sy_lo = min(sy_lo, __shfl_xor(sy_lo, m, 8));
+        sy_hi = max(sy_hi, __shfl_xor(sy_hi, m, 8));
+        ok = min(ok, __shfl_xor(ok, m, 8));
+    }
+    TileInfo t;
+    t.wd = Wd;
+    t.sxa = __builtin_amdgcn_readfirstlane(sx_lo) & ~15;
+    t.sya = __builtin_amdgcn_readfirstlane(sy_lo);
+    const int sxb = __builtin_amdgcn_readfirstlane(sx_hi), syb = __builtin_amdgcn_readfirstlane(sy_hi);
+    t.sw = sxb - t.sxa + 2;                    // bytes: columns sxa .. sxb + 1
+    t.sh = syb - t.sya + 2;                    // rows sya .. syb + 1
+    t.fast = __builtin_amdgcn_readfirstlane(ok) && t.sw > 0 && t.sh > 0 && t.sw <= kSP && t.sh <= kSH;
+    return t;
+}
+
+// LDS pointers stay 32-bit (address space 3) through the inlined helpers
+typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const d2v lds_d2;
+
+// raw buffer descriptor over [base, base + bytes): out-of-range loads return 0 and stores are
+// dropped, which is how lanes past the right edge and rows past the band go quiet.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, long long bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                             (int)min(bytes, (long long)0x7fffffff), 0x00020000);
+}
+
+// Fast-path rows of one lane: 4 columns x 8 rows (tile rows r0 + 8i).  xyp points at this lane's
+// (X0, Y0) of row r0 and block; tab8 at the weight table (entry f at byte 8f: (32-f, f), then
+// 64*(32-f, f)); src_base is the staged footprint.  g2 / mask go through buffer descriptors whose
+// per-lane offsets are out of range for idle lanes; ROWCHK (partial tiles) sends rows past the
+// band to row r0's coordinates so every tap stays inside the footprint.
+template <bool POW2, bool ROWCHK>
+__device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t src_base, int nvalid,
+                                          const uint32_t (&G)[kTH / 8],
+                                          __amdgpu_buffer_rsrc_t mrs, uint32_t moff, int ms, const double* tx,
+                                          const double* ty, double Wd, double mX, double mY, uint32_t bias)
+{
+#pragma unroll
+    for (int i = 0; i < kTH / 8; i++) {
+        const d2v xy = xyp[ROWCHK ? (i < nvalid ? 16 * i : 0) : 16 * i];   // rows are 2 blocks x 16 B apart
+        uint32_t xs_[4], ys_[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const double ax = xy.x + tx[k], ay = xy.y + ty[k];
+            double rx, ry;
+            if (POW2) {                                   // (X0 + M0*x1) * Wd exact: one rounding
+                rx = __builtin_fma(ax, Wd, mX);
+                ry = __builtin_fma(ay, Wd, mY);
+            } else {                                      // round the product, then to integer
+                rx = ax * Wd + mX;
+                ry = ay * Wd + mY;
+            }
+            xs_[k] = (uint32_t)__double2loint(rx);        // X - 32 * sxa
+            ys_[k] = (uint32_t)__double2loint(ry);        // Y - 32 * sya
+        }
+        uint32_t ad[4], wys[4], wxs[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            // 8X: byte 1 is the staged column (row), bits 3..7 index the 8-B weight table
+            const uint32_t lx = xs_[k] << 3, ly = ys_[k] << 3;
+            ad[k] = src_base + __builtin_amdgcn_perm(ly, lx, 0x0c0c0501u);   // (row << 8) | col
+            wys[k] = *(lds_u32*)(tab8 + (ly & 0xf8u));       // (32 - fy, fy)
+            wxs[k] = *(lds_u32*)(tab8 + (lx & 0xf8u) + 4);   // 64 * (32 - fx, fx)
+        }
+        // taps: four byte reads per pixel, c0 = (v00, v01), c1 = (v10, v11) as u16 halves.
+        // (ds_read_*_d16_hi does not preserve the low half on gfx950 with SRAM ECC, and unaligned
+        // ds_read_u16 is correct but ~4x slower here.)
+        uint32_t c0s[4], c1s[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            lds_u8* p = (lds_u8*)(uintptr_t)ad[k];
+            c0s[k] = (uint32_t)p[0] | ((uint32_t)p[1] << 16);
+            c1s[k] = (uint32_t)p[kSP] | ((uint32_t)p[kSP + 1] << 16);
+        }
+        uint32_t e[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u16x2v c0 = __builtin_bit_cast(u16x2v, c0s[k]), c1 = __builtin_bit_cast(u16x2v, c1s[k]);
+            const u16x2v wy = __builtin_bit_cast(u16x2v, wys[k]);
+            const u16x2v q = c0 * wy.xx + c1 * wy.yy;     // (q0, q1): vertical, exact in u16
+            const uint32_t s = __builtin_amdgcn_udot2(q, __builtin_bit_cast(u16x2v, wxs[k]), 32u, false);
+            const uint32_t g16 = __builtin_amdgcn_perm(0u, G[i], 0x0c000c0cu | ((uint32_t)k << 16));   // g_k << 16
+            asm("v_sad_u32 %0, %1, %2, %3" : "=v"(e[k]) : "v"(s), "v"(g16), "s"(bias));   // bit 31: moving
+        }
+        // v_perm selectors 9 / 11 replicate bit 31 of src1 / src0: 0xff or 0x00 bytes
+        const uint32_t out = __builtin_amdgcn_perm(e[1], e[0], 0x0c0c0b09u) | __builtin_amdgcn_perm(e[3], e[2], 0x0b090c0cu);
+        __builtin_amdgcn_raw_buffer_store_b32(out, mrs, (int)moff, i * ms, 0);
+    }
+}
+
+// staging: rows per pass and ceil(2^16 / nch) for nch = 1..16 chunks per footprint row
+__constant__ int kRowsPerPass[17] = {0, 256, 128, 85, 64, 51, 42, 36, 32, 28, 25, 23, 21, 19, 18, 17, 16};
+__constant__ uint32_t kInvChunks[17] = {0,     65536, 32768, 21846, 16384, 13108, 10923, 9363, 8192,
+                                        7282,  6554,  5958,  5462,  5042,  4682,  4370,  4096};
+
+// footprint chunks that cross the image's left / right edge: byte by byte, 0 outside (kept out of
+// line so its per-byte bounds are not computed on the interior path)
+__device__ __noinline__ void stage_edge_chunks(const uint8_t* src, int pitch, int w, int h, int sya, int sx, int ro,
+                                               int rpp, int sh, uint8_t* dst)
+{
+    for (int r = ro; r < sh; r += rpp) {
+        const int sy = sya + r;
+        uint32_t d[4] = {0, 0, 0, 0};
+        if ((unsigned)sy < (unsigned)h) {
+            const uint8_t* p = src + (long long)sy * pitch;
+            for (int i = 0; i < 16; i++) {
+                const int xx = sx + i;
+                if ((unsigned)xx < (unsigned)w) d[i >> 2] |= (uint32_t)p[xx] << (8 * (i & 3));
+            }
+        }
+        *reinterpret_cast<uint4*>(dst + r * kSP) = make_uint4(d[0], d[1], d[2], d[3]);
+    }
+}
+
+// grid: x -> tile column, y -> tile row of the band [row0, row1), z -> pair.  256 threads; lane l
+// of wave q owns columns x0 + 4*(l & 31) .. +3 of tile rows 2q + (l >> 5) + 8i, i = 0..7.  The
+// reference's blocking depends on the full height only through bw0, and each pixel's arithmetic
+// on (x, y) only, so a band is exactly the full frame's rows.
+__global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
+                                                   const uint8_t* __restrict__ g2, long long g2_stride, int g2_pitch,
+                                                   int w, int h, int bw0, const PairFit* __restrict__ fits,
+                                                   uint8_t* __restrict__ mask, long long mask_stride, int thresh,
+                                                   int vec_ok, int row0, int row1)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t s_tab[64];             // weight table
+    __shared__ __attribute__((aligned(16))) double s_xy[kTH][2][2];         // (X0, Y0) per row, block
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
+    __shared__ TileInfo s_info;
+
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs; remap the linear id so
+    // each XCD walks a contiguous run of tiles (row-major).  Horizontally adjacent tiles share the
+    // 128-B lines at their footprints' margins: in one L2 they are fetched once (PMC: 529 MB read
+    // per 4K x32 launch = 1.0x the algorithmic bytes; plain grid order, tiles of a row spread over
+    // the XCDs: 803 MB).
+    const int nbx = gridDim.x, nby = gridDim.y;
+    int bid = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+    {
+        const int total = nbx * nby * gridDim.z, xcd = bid & 7, q8 = total >> 3, r8 = total & 7;
+        bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    }
+    const int pair = bid / (nbx * nby), tile = bid - pair * (nbx * nby);
+    const int tx_ = tile % nbx, ty_ = tile / nbx;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int x0 = tx_ * kTW, y0 = row0 + ty_ * kTH;
+    const int cq = lane & 31;
+    const int xs = x0 + 4 * cq;                     // this lane's 4 columns
+    const int r0 = 2 * wave + (lane >> 5);          // this lane's first tile row (then every 8th)
+    const uint8_t* g2p = g2 + (long long)pair * g2_stride;
+    uint8_t* mp = mask + (long long)pair * mask_stride - (long long)row0 * w;   // indexed by frame row
+    // this lane's gray2 dwords, in flight from the start (their latency overlaps the staging)
+    const __amdgpu_buffer_rsrc_t g2rs = buf_rsrc(g2p, (long long)h * g2_pitch);
+    const uint32_t g2off = xs < w ? (uint32_t)((y0 + r0) * g2_pitch + xs) : 0x80000000u;
+    uint32_t G[kTH / 8];
+#pragma unroll
+    for (int i = 0; i < kTH / 8; i++) G[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * 8 * g2_pitch, 0);
+
+    const PairFit& f = fits[pair];
+    if (f.fit_status != 0) {   // no fit: the reference produces no mask; ours is all zero
+        const int nx = max(0, min(4, w - xs));
+        for (int r = r0; r < kTH && y0 + r < row1; r += 8) {
+            uint8_t* m = mp + (long long)(y0 + r) * w + xs;
+            for (int k = 0; k < nx; k++) m[k] = 0;
+        }
+        return;
+    }
+    double M[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) M[k] = f.Hinv[k];
+    const uint8_t* src = g1 + (long long)pair * g1_stride;
+    const bool affine = (M[6] == 0.0) && (M[7] == 0.0);
+    // fast path only over dword-aligned rows with reference blocks of 64 (uniform per workgroup)
+    const bool try_fast = affine && bw0 == kBW && vec_ok;
+
+    if (try_fast && wave == 0) {
+        const TileInfo t = tile_info(M, x0, y0, w, row1, lane);
+        if (lane == 0) s_info = t;
+    }
+    if (try_fast) __syncthreads();
+    const TileInfo t = s_info;
+    if (!try_fast || !t.fast) {
+        // ---- general path: per pixel, global gathers
+        const int nx = max(0, min(4, w - xs));
+        for (int r = r0; r < kTH && y0 + r < row1; r += 8) {
+            const int y = y0 + r;
+            const uint8_t* g2r = g2p + (long long)y * g2_pitch + xs;
+            uint8_t* m = mp + (long long)y * w + xs;
+            for (int k = 0; k < nx; k++) m[k] = warp_px_general(M, src, g1_pitch, w, h, xs + k, y, bw0, g2r[k], thresh);
+        }
+        return;
+    }
+
+    // ---- fast path: weight table, per-row X0/Y0 of both blocks, then stage the footprint
+    if (tid < 32) {
+        s_tab[2 * tid] = (uint32_t)(32 - tid) | ((uint32_t)tid << 16);
+        s_tab[2 * tid + 1] = (uint32_t)(64 * (32 - tid)) | ((uint32_t)(64 * tid) << 16);
+    }
+    if (tid < 2 * kTH) {
+        const int r = tid >> 1, b = tid & 1, y = y0 + r, xb = x0 + kBW * b;
+        s_xy[r][b][0] = M[0] * xb + M[1] * y + M[2];
+        s_xy[r][b][1] = M[3] * xb + M[4] * y + M[5];
+    }
+    if ((w & 15) == 0 && (g1_pitch & 3) == 0 && ((uintptr_t)src & 3) == 0) {
+        // LDS-DMA: every 16-B chunk is inside a row or wholly outside the image (w % 16 == 0,
+        // sxa a multiple of 16).  Wave-instruction I fills staged rows 4I..4I+3 (lane l: row
+        // 4I + l/16, chunk l%16); chunks outside the image read 0 through an out-of-range offset
+        // (BORDER_CONSTANT); nothing passes through VGPRs.
+        const __amdgpu_buffer_rsrc_t srs = buf_rsrc(src, (long long)h * g1_pitch);
+        const int ch = lane & 15, sx = t.sxa + 16 * ch;
+        const bool colin = sx >= 0 && sx < w;
+        const int nI = (t.sh + 3) >> 2, wvs = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+        for (int q = 0; q < (kSH + 15) / 16; q++) {
+            const int I = wvs + 4 * q;
+            if (I < nI) {
+                const int r = 4 * I + (lane >> 4);
+                const uint32_t off = colin ? (uint32_t)((t.sya + r) * g1_pitch + sx) : 0x80000000u;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, (__attribute__((address_space(3))) void*)&s_src[1024 * I],
+                                                         16, (int)off, 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the DMA (untracked by the compiler) landed
+        __builtin_amdgcn_sched_barrier(0);
+    } else {
+        // lane -> (row, 16-B chunk) of the footprint without an integer division: ro = tid / nch
+        // as a multiply by ceil(2^16 / nch) (exact for tid < 4096)
+        const int nch = (t.sw + 15) >> 4;                 // <= kSP / 16
+        const int rpp = kRowsPerPass[nch];                // 256 / nch rows per pass
+        const int ro = (int)(((uint32_t)tid * kInvChunks[nch]) >> 16), ch = tid - ro * nch;
+        const int sx = t.sxa + 16 * ch;
+        if (ro < rpp) {
+            if (sx >= 0 && sx + 16 <= w) {
+                // whole chunks inside the row: buffer loads, rows above / below the image fall
+                // outside the descriptor and read 0 (BORDER_CONSTANT)
+                const __amdgpu_buffer_rsrc_t srs = buf_rsrc(src, (long long)h * g1_pitch);
+                uint32_t off = (uint32_t)((t.sya + ro) * g1_pitch + sx);
+                const uint32_t step = (uint32_t)(rpp * g1_pitch);
+                for (int r = ro; r < t.sh; r += rpp, off += step) {
+                    const v4u v = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)off, 0, 0);
+                    *reinterpret_cast<uint4*>(&s_src[r * kSP + 16 * ch]) = make_uint4(v.x, v.y, v.z, v.w);
+                }
+            } else {
+                stage_edge_chunks(src, g1_pitch, w, h, t.sya, sx, ro, rpp, t.sh, &s_src[16 * ch]);
+            }
+        }
+    }
+    __syncthreads();
+
+    // lanes past the right edge compute on a valid column of block 0 and store nothing
+    const bool col_ok = xs < w;
+    const int cqe = col_ok ? cq : (cq & 15);
+    const int blk = cqe >> 4, x1b = 4 * (cqe & 15);
+    const double Wd = t.wd;                                  // computed once, by wave 0
+    const double magic = 6755399441055744.0;                 // 1.5 * 2^52: ulp 1
+    const double mX = magic - 32.0 * t.sxa, mY = magic - 32.0 * t.sya;
+    // 32/M8 a power of two -> (X0 + M0*x1) * Wd is exact and fuses with the rounding add
+    const bool pow2 = Wd != 0.0 && (__double_as_longlong(Wd) & 0x000fffffffffffffLL) == 0;
+    const int tc = min(max(thresh, -1), 255);                // t < 0: all moving; t >= 255: none
+    const uint32_t bias = 0x80000000u - (uint32_t)(65536 * tc + 32800);
+    double tx[4], ty[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        tx[k] = M[0] * (x1b + k);
+        ty[k] = M[3] * (x1b + k);
+        asm volatile("" : "+v"(tx[k]), "+v"(ty[k]));   // keep in registers (no per-row rematerialisation)
+    }
+    lds_d2* xyp = (lds_d2*)(&s_xy[r0][blk][0]);
+    lds_u8* tabp = (lds_u8*)(&s_tab[0]);
+    const uint32_t src_base = (uint32_t)(uintptr_t)(lds_u8*)(&s_src[0]);
+    // mask rows [0, row1) of the frame (stores past the band drop)
+    const __amdgpu_buffer_rsrc_t mrs = buf_rsrc(mp, (long long)row1 * w);
+    const uint32_t OOB = 0x80000000u;
+    const uint32_t moff = col_ok ? (uint32_t)((y0 + r0) * w + xs) : OOB;
+    const int nvalid = (row1 - y0 - r0 + 7) >> 3;            // rows r0 + 8i inside the band: i < nvalid
+    const bool rowchk = y0 + kTH > row1;
+    if (pow2) {
+        if (!rowchk)
+            warp_rows<true, false>(xyp, tabp, src_base, nvalid, G, mrs, moff, 8 * w, tx, ty, Wd,
+                                   mX, mY, bias);
+        else
+            warp_rows<true, true>(xyp, tabp, src_base, nvalid, G, mrs, moff, 8 * w, tx, ty, Wd,
+                                  mX, mY, bias);
+    } else {
+        warp_rows<false, true>(xyp, tabp, src_base, nvalid, G, mrs, moff, 8 * w, tx, ty, Wd, mX,
+                               mY, bias);
+    }
+}
+
+// ================================================================================================
+// Fixed-point coordinate variant (k_warp_fx).  Same tiling, staging and threshold as k_warp_diff;
+// the per-pixel FP64 coordinates and the LDS weight table are replaced by full-rate integer work:
+//
+//   U = Bx(row, block) + Lx(x1)   (mod 2^32),  layout [col: 24..31][fx: 19..23][fraction: 0..18]
+//   Bx = round(X0 * K) + 2^18 - 2^24 * sxa,  Lx(x1) = round(fl(M0 * x1) * K),  K = Wd * 2^19
+//
+// (X0 and fl(M0*x1) are the reference's doubles; both roundings are single FP64 FMAs against a
+// 1.5 * 2^52 magic constant, whose low word is the integer mod 2^32).  U differs from the real
+// R = fl(fl(X0 + fl(M0*x1)) * Wd) * 2^19 + 2^18 - 2^24 sxa by at most 1 + 2^-15 units (the
+// reference's own FP64 rounding errors are below 2^-16 units for |X| < 2^30), so U's bits 19..31
+// are cvRound(...) - 32 sxa unless U's fraction lies within 3 units of a rounding boundary.
+// Such "danger" (row, block) pairs are found per tile from a per-workgroup bitmap of the
+// fractions -Lx(j) - 3 (j = 0..63) at 64-unit buckets, confirmed by an exact wave-wide test, and
+// take the exact FP64 expression of k_warp_diff; every other pixel takes the integer path:
+//   tap address = v_perm(V, U) (row << 8 | col); P = V & 0xF80000 (= 8 fy << 16),
+//   Q = 2^24 - P (= (256 - 8 fy) << 16): vertical q8 = c0 * Q.hi + c1 * P.hi (packed u16, <= 65280);
+//   horizontal s = dot2(q8, (256 - 8 fx, 8 fx), 32) = 64 * Sum + 32, the same s as k_warp_diff.
+// ================================================================================================
+constexpr uint32_t kFxMask = 0x7ffffu;          // fraction bits of U
+constexpr int kFxDanger = 3;                    // danger half-width, units of 2^-19 (>= 1 + 2^-15, rounded up)
+
+__device__ __forceinline__ uint32_t fx_lo(double v) { return (uint32_t)__double2loint(v); }
+
+// exact reference coordinate of one pixel as a fixed-point word (fraction at mid-point)
+template <bool POW2>
+__device__ __forceinline__ uint32_t fx_exact(double a, double t, double Wd, int origin)
+{
+    const double s = a + t;
+    double r;
+    if (POW2) r = __builtin_fma(s, Wd, 6755399441055744.0);
+    else r = s * Wd + 6755399441055744.0;
+    return ((fx_lo(r) - 32u * (uint32_t)origin) << 19) | (1u << 18);
+}
+
+// exact FP64 coordinates of a lane's 4 pixels (rare: rows whose fixed-point fraction sits within
+// kFxDanger units of a rounding boundary)
+__device__ __forceinline__ void fx_exact_row(const double* __restrict__ Mg, int xb, int y, int x1b, double Wd, int pow2,
+                                          int sxa, int sya, uint32_t* U, uint32_t* V)
+{
+    const double X0 = Mg[0] * xb + Mg[1] * y + Mg[2];
+    const double Y0 = Mg[3] * xb + Mg[4] * y + Mg[5];
+    for (int k = 0; k < 4; k++) {
+        const double txk = Mg[0] * (double)(x1b + k), tyk = Mg[3] * (double)(x1b + k);
+        U[k] = pow2 ? fx_exact<true>(X0, txk, Wd, sxa) : fx_exact<false>(X0, txk, Wd, sxa);
+        V[k] = pow2 ? fx_exact<true>(Y0, tyk, Wd, sya) : fx_exact<false>(Y0, tyk, Wd, sya);
+    }
+}
+
+// Tile bounds of up to 8 vertically consecutive tiles at once: lane 8 tt + c evaluates corner c
+// of tile tt (as tile_info does per tile); group leaders write out[tt].
+__device__ void tile_info_strip(const double* M, int x0, int y0_first, int ntiles, int w, int yend, int lane,
+                                TileInfo* out)
+{
+    const int tt = lane >> 3, y0 = y0_first + kTH * tt;
+    const double Wd = M[8] != 0.0 ? 32.0 / M[8] : 0.0;
+    const int nb = (x0 + kBW < w) ? 2 : 1;
+    const int b = ((lane >> 2) & 1) < nb ? ((lane >> 2) & 1) : 0;
+    const int xb = x0 + kBW * b;
+    const int cxl = min(kBW - 1, w - 1 - xb), cyl = max(0, min(kTH - 1, yend - 1 - y0));
+    const int c = lane & 3;
+    const int x1 = (c & 1) ? cxl : 0, y = y0 + ((c & 2) ? cyl : 0);
+    const double X0 = M[0] * xb + M[1] * y + M[2];
+    const double Y0 = M[3] * xb + M[4] * y + M[5];
+    const double px = (X0 + M[0] * x1) * Wd, py = (Y0 + M[3] * x1) * Wd;
+    const double lim = 1073741824.0;   // 2^30
+    int ok = (px > -lim && px < lim && py > -lim && py < lim) ? 1 : 0;
+    int sx = 0, sy = 0;
+    if (ok) {
+        sx = ((int)__builtin_rint(px)) >> 5;
+        sy = ((int)__builtin_rint(py)) >> 5;
+    }
+    int sx_lo = sx, sx_hi = sx, sy_lo = sy, sy_hi = sy;
+#pragma unroll
+    for (int m = 1; m <= 4; m <<= 1) {
+        sx_lo = min(sx_lo, __shfl_xor(sx_lo, m, 8));
+        sx_hi = max(sx_hi, __shfl_xor(sx_hi, m, 8));
+        sy_lo = min(sy_lo, __shfl_xor(sy_lo, m, 8));
+        sy_hi = max(sy_hi, __shfl_xor(sy_hi, m, 8));
+        ok = min(ok, __shfl_xor(ok, m, 8));
+    }
+    if ((lane & 7) == 0 && tt < ntiles) {
+        TileInfo t;
+        t.wd = Wd;
+        t.sxa = sx_lo & ~15;
+        t.sya = sy_lo;
+        t.sw = sx_hi - t.sxa + 2;
+        t.sh = sy_hi - t.sya + 2;
+        t.fast = ok && t.sw > 0 && t.sh > 0 && t.sw <= kSP && t.sh <= kSH;
+        out[tt] = t;
+    }
+}
+
+constexpr int kStrip = 8;   // tiles per workgroup at most (a vertical strip of one tile column)
+
+// Persistent over a vertical strip of up to kStrip tiles of one pair.  Per tile n, one barrier:
+//   issue mask stores of tile n-1 | LDS-DMA of tile n+1's footprint + its gray2 dwords |
+//   row bases of tile n+1 (two waves, alternating) | rows of tile n | vmcnt(0), barrier.
+// The strip's tile bounds come from one wave in the prologue, with the danger buckets and the
+// per-lane column constants.  Requires w % 16 == 0 and dword-aligned rows (launcher checks).
+__global__ __launch_bounds__(256) void k_warp_fx(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
+                                                 const uint8_t* __restrict__ g2, long long g2_stride, int g2_pitch,
+                                                 int w, int h, const PairFit* __restrict__ fits,
+                                                 uint8_t* __restrict__ mask, long long mask_stride, int thresh,
+                                                 int row0, int row1, int nstrips, int strip_tiles)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[2][kSH * kSP];
+    __shared__ __attribute__((aligned(16))) uint32_t s_base[kStrip][kTH][2][2];   // (Bx, By) per tile, row, block
+    __shared__ __attribute__((aligned(16))) uint32_t s_bm[2][256];           // danger buckets (x, y)
+    __shared__ unsigned long long s_dng[kStrip][2];                                // danger (row, block) bits
+    __shared__ TileInfo s_info[kStrip];
+
+    const int nbx = gridDim.x, nby = nstrips;
+    int bid = blockIdx.x + nbx * (blockIdx.y + nby * blockIdx.z);
+    {
+        const int total = nbx * nby * gridDim.z, xcd = bid & 7, q8 = total >> 3, r8 = total & 7;
+        bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    }
+    const int pair = bid / (nbx * nby), rem = bid - pair * (nbx * nby);
+    const int tx_ = rem % nbx, strip = rem / nbx;
+    const int nty = (row1 - row0 + kTH - 1) / kTH;
+    const int ty0 = strip * strip_tiles, ntiles = min(strip_tiles, nty - ty0);
+    if (ntiles <= 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int x0 = tx_ * kTW;
+    const int cq = lane & 31;
+    const int xs = x0 + 4 * cq;
+    const int r0 = 2 * wave + (lane >> 5);
+    const bool col_ok = xs < w;
+    const uint8_t* g2p = g2 + (long long)pair * g2_stride;
+    uint8_t* mp = mask + (long long)pair * mask_stride - (long long)row0 * w;
+    const uint8_t* src = g1 + (long long)pair * g1_stride;
+
+    const PairFit& f = fits[pair];
+    double M[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) M[k] = f.Hinv[k];
+    const bool affine = (M[6] == 0.0) && (M[7] == 0.0);
+    if (f.fit_status != 0 || !affine) {   // no fit: zero mask; perspective: exact per-pixel path
+        const int nx = max(0, min(4, w - xs));
+        for (int tt = 0; tt < ntiles; tt++) {
+            const int y0 = row0 + (ty0 + tt) * kTH;
+            for (int r = r0; r < kTH && y0 + r < row1; r += 8) {
+                const int y = y0 + r;
+                const uint8_t* g2r = g2p + (long long)y * g2_pitch + xs;
+                uint8_t* m = mp + (long long)y * w + xs;
+                for (int k = 0; k < nx; k++)
+                    m[k] = f.fit_status != 0 ? 0 : warp_px_general(M, src, g1_pitch, w, h, xs + k, y, kBW, g2r[k], thresh);
+            }
+        }
+        return;
+    }
+
+    const double Wd = M[8] != 0.0 ? 32.0 / M[8] : 0.0;
+    const double K = Wd * 524288.0;                              // Wd * 2^19 (exact)
+    const double magic = 6755399441055744.0;                     // 1.5 * 2^52: ulp 1
+    const bool pow2 = Wd != 0.0 && (__double_as_longlong(Wd) & 0x000fffffffffffffLL) == 0;
+
+    // ---- prologue: clear the danger buckets, strip tile bounds (wave 0), lane constants
+    for (int i = tid; i < 512; i += 256) (&s_bm[0][0])[i] = 0u;
+    if (wave == 0) tile_info_strip(M, x0, row0 + ty0 * kTH, ntiles, w, row1, lane, s_info);
+    // lane j: L_x(j), L_y(j) (the exact danger test); lane's columns: L_x(x1b + k), L_y(x1b + k)
+    const uint32_t lxj = fx_lo(__builtin_fma(M[0] * (double)lane, K, magic));
+    const uint32_t lyj = fx_lo(__builtin_fma(M[3] * (double)lane, K, magic));
+    const int cqe = col_ok ? cq : (cq & 15);
+    const int blk = cqe >> 4, x1b = 4 * (cqe & 15);
+    uint32_t Lx[4], Ly[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        Lx[k] = fx_lo(__builtin_fma(M[0] * (double)(x1b + k), K, magic));
+        Ly[k] = fx_lo(__builtin_fma(M[3] * (double)(x1b + k), K, magic));
+    }
+    const int tc = min(max(thresh, -1), 255);
+    const uint32_t bias = 0x80000000u - (uint32_t)(65536 * tc + 32800);
+    __syncthreads();
+    // danger buckets: wave 0 x axis, wave 1 y axis; fractions -L(j) - 3 .. +2, 64-unit buckets
+    if (wave < 2) {
+        const uint32_t lam = (wave ? lyj : lxj) & kFxMask;
+        const uint32_t s0 = (0u - lam - (uint32_t)kFxDanger) & kFxMask, s1 = (s0 + 2 * kFxDanger - 1) & kFxMask;
+        atomicOr(&s_bm[wave][(s0 >> 6) >> 5], 1u << ((s0 >> 6) & 31));
+        atomicOr(&s_bm[wave][(s1 >> 6) >> 5], 1u << ((s1 >> 6) & 31));
+    }
+
+    const __amdgpu_buffer_rsrc_t srs = buf_rsrc(src, (long long)h * g1_pitch);
+    const __amdgpu_buffer_rsrc_t g2rs = buf_rsrc(g2p, (long long)h * g2_pitch);
+    const __amdgpu_buffer_rsrc_t mrs = buf_rsrc(mp, (long long)row1 * w);
+    const uint32_t OOB = 0x80000000u;
+    const int ch = lane & 15;
+
+    // staging of tile tt into buffer b: LDS-DMA (wave-instruction I fills staged rows 4I..4I+3),
+    // chunks outside the image read 0 through an out-of-range offset; plus this lane's gray2 dwords
+    auto prefetch = [&](int tt, int b, uint32_t (&Gd)[kTH / 8]) {
+        const TileInfo t = s_info[tt];
+        const int y0 = row0 + (ty0 + tt) * kTH;
+        const uint32_t g2off = col_ok ? (uint32_t)((y0 + r0) * g2_pitch + xs) : OOB;
+#pragma unroll
+        for (int i = 0; i < kTH / 8; i++) Gd[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * 8 * g2_pitch, 0);
+        if (!t.fast) return;
+        const int sx = t.sxa + 16 * ch;
+        const bool colin = sx >= 0 && sx < w;
+        const int nI = (t.sh + 3) >> 2;
+#pragma unroll
+        for (int q = 0; q < (kSH + 15) / 16; q++) {
+            const int I = wv + 4 * q;
+#ifdef WX_NODMA   // TEMP timing-only
+            if (I < 0) {
+#else
+            if (I < nI) {
+#endif
+                const int r = 4 * I + (lane >> 4);
+                const uint32_t off = colin ? (uint32_t)((t.sya + r) * g1_pitch + sx) : OOB;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, (__attribute__((address_space(3))) void*)&s_src[b][1024 * I],
+                                                         16, (int)off, 0, 0, 0);
+            }
+        }
+    };
+    // row bases (Bx, By) and danger bits of every tile of the strip, once: wave w takes tiles
+    // tt = w/2, w/2 + 2, ...; lane -> (row, block) = (32 (w & 1) + lane/2, lane & 1); candidate
+    // rows from the buckets are confirmed by the exact wave-wide test
+    auto bases = [&](int tt) {
+        const TileInfo t = s_info[tt];
+        if (!t.fast) return;
+        const int half = wv & 1, r = 32 * half + (lane >> 1), bb = lane & 1;
+        // rows past the band take the band's last row: in the footprint, their stores drop
+        const int y = min(row0 + (ty0 + tt) * kTH + r, row1 - 1), xb = x0 + kBW * bb;
+        const double X0 = M[0] * xb + M[1] * y + M[2];
+        const double Y0 = M[3] * xb + M[4] * y + M[5];
+        const double cX = magic + (double)(1 << 18) - 16777216.0 * (double)t.sxa;
+        const double cY = magic + (double)(1 << 18) - 16777216.0 * (double)t.sya;
+        const uint32_t Bx = fx_lo(__builtin_fma(X0, K, cX)), By = fx_lo(__builtin_fma(Y0, K, cY));
+        *reinterpret_cast<uint2*>(&s_base[tt][r][bb][0]) = make_uint2(Bx, By);
+        const uint32_t ux = (Bx & kFxMask) >> 6, uy = (By & kFxMask) >> 6;
+        const bool cand = ((s_bm[0][ux >> 5] >> (ux & 31)) & 1u) | ((s_bm[1][uy >> 5] >> (uy & 31)) & 1u);
+        unsigned long long cm = __ballot(cand), dm = 0ull;
+        while (cm) {   // rare: wave-wide exact test of one candidate (lane j: L(j))
+            const int sl = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            const uint32_t bx = (uint32_t)__shfl((int)Bx, sl), by = (uint32_t)__shfl((int)By, sl);
+            const bool dx = ((bx + lxj + (uint32_t)kFxDanger) & kFxMask) < (uint32_t)(2 * kFxDanger);
+            const bool dy = ((by + lyj + (uint32_t)kFxDanger) & kFxMask) < (uint32_t)(2 * kFxDanger);
+            if (__ballot(dx || dy) != 0ull) dm |= 1ull << sl;
+        }
+        if (lane == 0) s_dng[tt][half] = dm;
+    };
+
+    uint32_t G[kTH / 8], Gn[kTH / 8], O[kTH / 8];
+    prefetch(0, 0, G);
+    __syncthreads();          // buckets marked
+    for (int tt = wv >> 1; tt < ntiles; tt += 2) bases(tt);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): tile 0's DMA landed (untracked by the compiler)
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+
+    uint32_t moff_prev = OOB;
+    // tile n uses buffer n & 1; the body is instantiated per buffer so LDS offsets are immediates
+    auto tile = [&](int n, auto bc) {
+        constexpr int b = decltype(bc)::value;
+        const int y0 = row0 + (ty0 + n) * kTH;
+        // mask rows of the previous tile (stored now so the barrier's vmcnt(0) finds them done)
+        if (n > 0) {
+#pragma unroll
+            for (int i = 0; i < kTH / 8; i++) __builtin_amdgcn_raw_buffer_store_b32(O[i], mrs, (int)moff_prev, i * 8 * w, 0);
+        }
+        if (n + 1 < ntiles) {
+            prefetch(n + 1, b ^ 1, Gn);
+        }
+        const TileInfo t = s_info[n];
+        const uint32_t moff = col_ok ? (uint32_t)((y0 + r0) * w + xs) : OOB;
+        if (!t.fast) {   // exact per-pixel path for this tile (huge / far-away footprint)
+            const int nx = max(0, min(4, w - xs));
+            for (int r = r0; r < kTH && y0 + r < row1; r += 8) {
+                const int y = y0 + r;
+                const uint8_t* g2r = g2p + (long long)y * g2_pitch + xs;
+                uint8_t* m = mp + (long long)y * w + xs;
+                for (int k = 0; k < nx; k++) m[k] = warp_px_general(M, src, g1_pitch, w, h, xs + k, y, kBW, g2r[k], thresh);
+            }
+#pragma unroll
+            for (int i = 0; i < kTH / 8; i++) O[i] = 0u;
+            moff_prev = OOB;
+        } else {
+            const unsigned long long d0 = s_dng[n][0], d1 = s_dng[n][1];
+            const unsigned long long D0 = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(d0 >> 32)) << 32) |
+                                          __builtin_amdgcn_readfirstlane((uint32_t)d0);
+            const unsigned long long D1 = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(d1 >> 32)) << 32) |
+                                          __builtin_amdgcn_readfirstlane((uint32_t)d1);
+            // iterations i whose rows 2 wv + {0, 1} + 8 i (past the band: row r0) have a danger block
+            uint32_t itm = 0;
+#pragma unroll
+            for (int i = 0; i < kTH / 8; i++) {
+                const int ra = 2 * wv + 8 * i;
+                if ((((ra >> 5) ? D1 : D0) >> (2 * (ra & 31))) & 15ull) itm |= 1u << i;
+            }
+            itm = __builtin_amdgcn_readfirstlane(itm);
+            const uint32_t src_base = (uint32_t)(uintptr_t)(lds_u8*)(&s_src[b][0]);
+            // one row of 4 pixels from fixed-point coordinates U, V -> 4 mask bytes
+            auto row_out = [&](const uint32_t (&U)[4], const uint32_t (&V)[4], uint32_t Gi) -> uint32_t {
+                uint32_t e[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t ad = src_base + __builtin_amdgcn_perm(V[k], U[k], 0x0c0c0703u);   // (row << 8) | col
+                    lds_u8* p = (lds_u8*)(uintptr_t)ad;
+                    const uint32_t c0s = (uint32_t)p[0] | ((uint32_t)p[1] << 16);
+                    const uint32_t c1s = (uint32_t)p[kSP] | ((uint32_t)p[kSP + 1] << 16);
+                    // fraction bytes of U, V in the u16 halves: (8 fx, 8 fy), and (256 - 8 fx, 256 - 8 fy)
+                    const uint32_t F = __builtin_amdgcn_perm(V[k], U[k], 0x0c060c02u) & 0x00f800f8u;
+                    const u16x2v Fv = __builtin_bit_cast(u16x2v, F), Gv = (u16x2v){256, 256} - Fv;
+                    const uint32_t wx = __builtin_amdgcn_perm(F, __builtin_bit_cast(uint32_t, Gv), 0x05040100u);
+                    const u16x2v c0 = __builtin_bit_cast(u16x2v, c0s), c1 = __builtin_bit_cast(u16x2v, c1s);
+                    const u16x2v q = c0 * Gv.yy + c1 * Fv.yy;                    // vertical, <= 65280
+                    const uint32_t s = __builtin_amdgcn_udot2(q, __builtin_bit_cast(u16x2v, wx), 32u, false);
+                    const uint32_t g16 = __builtin_amdgcn_perm(0u, Gi, 0x0c000c0cu | ((uint32_t)k << 16));
+                    asm("v_sad_u32 %0, %1, %2, %3" : "=v"(e[k]) : "v"(s), "v"(g16), "s"(bias));
+                }
+                return __builtin_amdgcn_perm(e[1], e[0], 0x0c0c0b09u) | __builtin_amdgcn_perm(e[3], e[2], 0x0b090c0cu);
+            };
+            // every row on the integer path, branch-free (the rows interleave freely) ...
+#pragma unroll
+            for (int i = 0; i < kTH / 8; i++) {
+                const int rr = r0 + 8 * i;   // rows past the band hold the band's last row (bases)
+                const uint2 bxy = *reinterpret_cast<const uint2*>(&s_base[n][rr][blk][0]);
+#ifdef WX_MEMONLY   // TEMP timing-only
+                O[i] = G[i] ^ bxy.x ^ bxy.y;
+                continue;
+#endif
+                uint32_t U[4], V[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    U[k] = bxy.x + Lx[k];
+                    V[k] = bxy.y + Ly[k];
+                }
+                O[i] = row_out(U, V, G[i]);
+            }
+            // ... then, rarely, the danger rows again from exact FP64 coordinates
+            if (itm) {
+                for (int i = 0; i < kTH / 8; i++) {
+                    const int rr = r0 + 8 * i;
+                    const unsigned long long Dm = (rr >> 5) ? D1 : D0;
+                    if (((itm >> i) & 1u) && ((Dm >> (2 * (rr & 31) + blk)) & 1ull)) {
+                        uint32_t U[4], V[4];
+                        fx_exact_row(f.Hinv, x0 + kBW * blk, min(y0 + rr, row1 - 1), x1b, Wd, pow2, t.sxa, t.sya, U, V);
+                        uint32_t Gi = G[0];
+#pragma unroll
+                        for (int j = 1; j < kTH / 8; j++) Gi = j == i ? G[j] : Gi;
+                        const uint32_t o = row_out(U, V, Gi);
+#pragma unroll
+                        for (int j = 0; j < kTH / 8; j++) O[j] = j == i ? o : O[j];
+                    }
+                }
+            }
+            moff_prev = moff;
+        }
+        if (n + 1 < ntiles) {
+#pragma unroll
+            for (int i = 0; i < kTH / 8; i++) G[i] = Gn[i];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the next tile's DMA landed
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+    };
+    for (int n = 0; n < ntiles; n += 2) {
+        tile(n, std::integral_constant<int, 0>{});
+        if (n + 1 < ntiles) tile(n + 1, std::integral_constant<int, 1>{});
+    }
+#pragma unroll
+    for (int i = 0; i < kTH / 8; i++) __builtin_amdgcn_raw_buffer_store_b32(O[i], mrs, (int)moff_prev, i * 8 * w, 0);
+}
+
+static int warp_impl()
+{
+    static int impl = -1;
+    if (impl < 0) {
+        const char* e = std::getenv("MDX_WARP");
+        impl = (e && std::atoi(e) == 2) ? 2 : 1;
+    }
+    return impl;
+}
+
+hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,
+                            const uint8_t* g2, long long g2_stride, int g2_pitch, int w, int h, const PairFit* fits,
+                            uint8_t* mask, long long mask_stride, int thresh, int row0, int row1)
+{
+    if (row1 < 0) row1 = h;
+    if (row0 < 0 || row1 > h || row0 >= row1) return hipErrorInvalidValue;
+    {
+        const int bh0 = h < 16 ? h : 16;
+        const int bw0 = (1024 / bh0) < w ? (1024 / bh0) : w;
+        // fixed-point strip kernel: reference blocks of 64, 16-B footprint chunks never straddle
+        // the image edge (w % 16 == 0), dword-aligned rows for the DMA, gray2 loads, mask stores
+        const bool fx_ok = warp_impl() == 2 && bw0 == kBW && w % 16 == 0 && ((uintptr_t)g1 % 4 == 0) &&
+                           g1_stride % 4 == 0 && g1_pitch % 4 == 0 && ((uintptr_t)g2 % 4 == 0) && g2_stride % 4 == 0 &&
+                           g2_pitch % 4 == 0 && ((uintptr_t)mask % 4 == 0) && mask_stride % 4 == 0;
+        if (fx_ok) {
+            const int nty = (row1 - row0 + kTH - 1) / kTH;
+            const int nstrips = (nty + kStrip - 1) / kStrip, strip_tiles = (nty + nstrips - 1) / nstrips;
+            const dim3 grid((w + kTW - 1) / kTW, nstrips, batch);
+            hipLaunchKernelGGL(k_warp_fx, grid, dim3(256), 0, s, g1, g1_stride, g1_pitch, g2, g2_stride, g2_pitch, w, h,
+                               fits, mask, mask_stride, thresh, row0, row1, nstrips, strip_tiles);
+            return hipGetLastError();
+        }
+    }
+    if (row1 < 0) row1 = h;
+    if (row0 < 0 || row1 > h || row0 >= row1) return hipErrorInvalidValue;
+    const int bh0 = h < 16 ? h : 16;
+    const int bw0 = (1024 / bh0) < w ? (1024 / bh0) : w;
+    // dword loads of gray2 / stores of the mask need 4-B aligned rows
+    const int vec_ok = ((uintptr_t)g2 % 4 == 0) && g2_stride % 4 == 0 && g2_pitch % 4 == 0 &&
+                       ((uintptr_t)mask % 4 == 0) && mask_stride % 4 == 0 && w % 4 == 0;
+    const dim3 grid((w + kTW - 1) / kTW, (row1 - row0 + kTH - 1) / kTH, batch);
+    hipLaunchKernelGGL(k_warp_diff, grid, dim3(256), 0, s, g1, g1_stride, g1_pitch, g2, g2_stride, g2_pitch, w, h, bw0,
+                       fits, mask, mask_stride, thresh, vec_ok, row0, row1);
+    return hipGetLastError();
+}
+
+}  // namespace mdx

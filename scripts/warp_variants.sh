@@ -10,6 +10,6 @@ for v in "$@"; do
     name=${v%%:*}; defs=${v#*:}
     $H $F $defs -c mdx_warp.hip -o ../build/var/warp_$name.o
     $H --offload-arch=gfx950 -shared -fPIC -pthread ../build/mdx_kernels.o ../build/mdx_lk.o ../build/mdx_subspace.o ../build/var/warp_$name.o \
-        ../build/mdx_api.o ../build/synth.o -o ../lib/libmdx_$name.so
+        ../build/mdx_api.o ../build/synth.o ../build/buildinfo.o -o ../lib/libmdx_$name.so
     echo "built libmdx_$name.so ($defs)"
 done

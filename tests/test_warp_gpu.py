@@ -38,6 +38,11 @@ def _H(kind, w, h, Ht):
         "m8_not_pow2": np.array([[1.01, 0.002, 3.2], [-0.003, 0.99, -1.7], [0.0, 0.0, 1.3]]),
         "projective": np.array([[1.002, 0.013, -2.5], [-0.011, 0.995, 1.75], [2.1e-5, -1.3e-5, 1.0]]),
         "singular": np.zeros((3, 3)),
+        # fixed-point screening (k_warp_fx): rows y = 32 mod 64 sit exactly on rounding ties
+        # (X = 32 x + y / 64), the others 1/64 px away; and coordinates 2^-23 px past a tie
+        "tie_rows": np.array([[1.0, 1.0 / 2048, 0.0], [0.0, 1.0, 0.0], [0.0, 0.0, 1.0]]),
+        "near_tie": np.array([[1.0, 0.0, 0.5 / 32 + 2.0 ** -28], [0.0, 1.0, -0.5 / 32 - 2.0 ** -29], [0.0, 0.0, 1.0]]),
+        "near_tie_rot": _rot(0.25, 1.0, 0.5 / 32 + 2.0 ** -27, 0.5 / 32 - 2.0 ** -26, w / 2, h / 2),
     }[kind]
 
 
@@ -71,7 +76,7 @@ def _run(mdx, ctx, oracle, g1, g2, Hs, thresh):
 
 
 KINDS = ["true", "identity", "tie_translation", "tie_scale_half", "rot5", "flip_x", "zoom_in", "zoom_out",
-         "far_away", "m8_not_pow2", "projective", "singular"]
+         "far_away", "m8_not_pow2", "projective", "singular", "tie_rows", "near_tie", "near_tie_rot"]
 
 
 @pytest.mark.parametrize("w,h", [(640, 480), (1000, 300), (1984, 70), (128, 64), (132, 65), (68, 33)])
