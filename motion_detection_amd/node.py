@@ -7,9 +7,9 @@ encoding, step, data).  Parameters mirror the node's ROS params (:29-44, :237-24
 
 * skip_frames (default 1) and num_motions (default 2) are re-read on every frame;
   trajectory_size = 2*num_motions + 1, or 2 when egomotion is false (:241-245).
-* a frame is dropped unless global_frame_count % skip_frames == 0 (:247).  Like the
-  reference, the counter only advances on dropped frames, so skip_frames > 1 keeps every
-  frame once the counter is a multiple of skip_frames; the mirror keeps that quirk.
+* a frame is dropped unless global_frame_count % skip_frames == 0 (:247).  The counter
+  advances on every call: on a dropped frame at :247, on a kept one at :454 (:315 when no
+  trajectory survives), so skip_frames = k keeps frames 0, k, 2k, ...
 * raw frames go into a ring of trajectory_size (:248-261); once full, the last two
   frames are converted to rgb8 (cv_bridge toCvCopy, :271) and handed to the calculator.
 
@@ -78,8 +78,11 @@ class LiveResult:
 
 class MotionDetectionNode:
     def __init__(self, params: dict | None = None, on_result: Callable | None = None, device: int = 0):
+        # the reference's defaults (node.cpp:29-44, :237-240, :346); egomotion true (:40) sets a
+        # ring of 2*num_motions+1 frames.  live_chain=False (the pair path) is this mirror's own
+        # default: the reference's imageCallback always runs the live branch.
         self.params = {"pixel_step": 10, "min_vector_size": 1.0, "skip_frames": 1, "num_motions": 2,
-                       "egomotion": False, "use_all_frames": True, "sigma": 0.5, "live_chain": False}
+                       "egomotion": True, "use_all_frames": True, "sigma": 0.5, "live_chain": False}
         if params:
             self.params.update(params)
         self.on_result = on_result
@@ -110,12 +113,15 @@ class MotionDetectionNode:
             self.raw_images.append(msg)
             self.raw_images.popleft()
             self.image_received = True
-        if not (self.params.get("use_all_frames", True) and self.image_received):
-            return None
-        if self.params.get("live_chain", False):
-            return self.run_live_chain([to_rgb8(m) for m in self.raw_images])   # :266-295
-        frames = [to_rgb8(m) for m in list(self.raw_images)[-2:]]   # :266-287
-        return self.run_optical_flow(frames[0], frames[1])
+        out = None
+        if self.params.get("use_all_frames", True) and self.image_received:
+            if self.params.get("live_chain", False):
+                out = self.run_live_chain([to_rgb8(m) for m in self.raw_images])   # :266-295
+            else:
+                frames = [to_rgb8(m) for m in list(self.raw_images)[-2:]]   # :266-287
+                out = self.run_optical_flow(frames[0], frames[1])
+        self.global_frame_count += 1                          # :454
+        return out
 
     def run_live_chain(self, images: list):
         """runOpticalFlowTrajectory (node.cpp:94-110) then, with egomotion, fitSubspace (:341-348)."""

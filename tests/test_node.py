@@ -55,7 +55,7 @@ def test_to_rgb8_conversions():
 
 
 def test_pairs_of_consecutive_frames():
-    n = make_node()
+    n = make_node(egomotion=False)
     assert n.trajectory_size == 2
     assert n.image_callback(frame(10)) is None            # ring not yet full
     assert n.image_callback(frame(20)) == 1
@@ -65,6 +65,12 @@ def test_pairs_of_consecutive_frames():
     assert a1.shape == (6, 8, 3) and fmt == m.FMT_RGB8      # cv_bridge rgb8 copy (node.cpp:271)
     assert (ps, mvs) == (10, 1.0)
     assert n.frames_processed == 2
+
+
+def test_reference_defaults():
+    n = make_node()
+    assert n.params["egomotion"] is True                     # node.cpp:40
+    assert n.trajectory_size == 5                            # 2*num_motions + 1 (:241)
 
 
 def test_egomotion_ring_size():
@@ -77,19 +83,14 @@ def test_egomotion_ring_size():
     assert a[0, 0, 0] == 3 and b[0, 0, 0] == 4              # the last two frames of the ring
 
 
-def test_skip_frames_quirk():
-    # node.cpp:247: the counter only advances on dropped frames, so once it is a multiple of
-    # skip_frames every later frame is kept
-    n = make_node(skip_frames=3)
-    for v in range(6):
-        n.image_callback(frame(v))
-    assert n.global_frame_count == 0                        # 0 % 3 == 0: nothing is ever dropped
-    assert len(n.ofc.calls) == 5
-    n = make_node(skip_frames=3)
-    n.global_frame_count = 1
-    out = [n.image_callback(frame(v)) for v in range(6)]
-    assert out[:2] == [None, None] and n.global_frame_count == 3
-    assert len(n.ofc.calls) == 3                            # frames 2..5 kept -> 3 pairs
+def test_skip_frames():
+    # node.cpp:247 drops a frame unless the counter is a multiple of skip_frames; the counter
+    # advances on every call (:247 dropped, :454 kept), so frames 0, 3, 6, ... are kept
+    n = make_node(skip_frames=3, egomotion=False)
+    out = [n.image_callback(frame(v)) for v in range(10)]
+    assert n.global_frame_count == 10
+    assert [i for i, o in enumerate(out) if o is not None] == [3, 6, 9]   # pairs (0,3), (3,6), (6,9)
+    assert [(c[0][0, 0, 0], c[1][0, 0, 0]) for c in n.ofc.calls] == [(0, 3), (3, 6), (6, 9)]
 
 
 def test_use_all_frames_false_never_runs():
@@ -176,7 +177,7 @@ def test_live_chain_trajectory_and_subspace():
     assert rec.fit_calls == [(3, 2, 0.7)]
     assert res.num_vectors == 7 and res.outlier_points == [(1.0, 2.0)] and len(res.subspace) == 1
     # without egomotion: trajectories only (the reference clusters them instead, out of scope)
-    n2 = MotionDetectionNode({"live_chain": True})
+    n2 = MotionDetectionNode({"live_chain": True, "egomotion": False})
     rec2 = RecordingLive()
     n2.ofc = rec2
     n2.od = rec2
