@@ -187,6 +187,7 @@ def test_node_pair_path_matches_oracle(node_exe, tmp_path, mdx, oracle, enc, ski
     kept = kept_frames(len(frames), skip)
     ring_pairs = [(kept[i - 1], kept[i]) for i in range(1, len(kept))]   # trajectory_size 2
     assert f"processed {len(ring_pairs)} of {len(frames)}" in p.stdout, p.stdout
+    log_lines = []
     for k, (i1, i2) in enumerate(ring_pairs):
         f1, f2 = to_rgb8(seq[i1], enc), to_rgb8(seq[i2], enc)
         ref = oracle.calculate_optical_flow(f1, f2, pixel_step=ps, min_vector_size=mvs)
@@ -213,7 +214,10 @@ def test_node_pair_path_matches_oracle(node_exe, tmp_path, mdx, oracle, enc, ski
         write_flow(vi, pyf, ps)
         for sfx in ("_h", "_f"):
             assert open(out / f"flow_{k}{sfx}", "rb").read() == open(pyf + sfx, "rb").read()
-    assert os.path.getsize(out / "motion.log") > 0
+        ys, xs = np.nonzero(ref["mask"])
+        if len(ys):   # MotionLogger::writeBoundingBox of the moving pixels' box (frame = counter at the call)
+            log_lines.append(f"{i2}, 0, {xs.min()}, {ys.min()}, {xs.max() + 1}, {ys.max() + 1}")
+    assert open(out / "motion.log").read().splitlines() == log_lines
 
 
 @pytest.mark.gpu
