@@ -144,6 +144,49 @@ def cpu_baseline(uniq, w, h, seconds: float, threads: int):
 REHEARSE = False   # --rehearse: ranks beyond the visible devices may share device 0
 
 
+VALU_PEAK_WAVE_INSTR = 1024 * 2.4e9 / 4   # 1024 SIMDs x 2.4 GHz, one wave64 VALU instruction per 4 cycles
+LK_VALU_PER_ELEM_ITER = 5   # minimal per window element and Newton iteration: 2 v_dot2 (bilinear J, folded I),
+                            # 1 cvt, 1 v_pk_mul_f32 + 1 v_pk_add_f32 (b1, b2 products rounded before the add)
+LK_VALU_PER_ELEM_A = 2      # minimal per element of the gradient sums: 1 v_pk_fma_f32 + 1 v_fma_f32 (A11/A22, A12)
+
+
+def lk_levels(w: int, h: int, max_level: int = 5, win: int = 40) -> int:
+    """Pyramid levels the LK runs (buildOpticalFlowPyramid stops when a side would be <= win)."""
+    L = 0
+    while L < max_level and (w + 1) // 2 > win and (h + 1) // 2 > win:
+        w, h, L = (w + 1) // 2, (h + 1) // 2, L + 1
+    return L + 1
+
+
+def lk_work(dev: int, w: int, h: int, ps: int, uniq) -> dict:
+    """Per-point Newton iterations of the pyramidal LK on the bench's distinct pairs, from the
+    kernel's own per-(level, point) trace (MDX_LK_DEBUG context, untimed).  Returns the
+    algorithmic VALU lane-instructions per pair: 1600 window elements x (LK_VALU_PER_ELEM_A per
+    tracked (level, point) + LK_VALU_PER_ELEM_ITER per executed iteration)."""
+    import ctypes as C
+    os.environ["MDX_LK_DEBUG"] = "1"
+    try:
+        ctx = mdx.Context(dev, w, h, 1, pixel_step=ps, min_vector_size=1.0)
+    finally:
+        del os.environ["MDX_LK_DEBUG"]
+    n, nl = mdx.grid_count(w, h, ps), lk_levels(w, h)
+    its, trk = [], []
+    for a, b, _ in uniq:
+        ctx.flow_warp_diff(a, b)
+        buf = np.zeros((nl, n, 4), np.float32)
+        rc = mdx.lib().mdx_debug_copy(ctx._h, 1, buf.ctypes.data_as(C.c_void_p), buf.nbytes)
+        if rc != 0:
+            raise mdx.MdxError(f"mdx_debug_copy rc {rc}")
+        it = buf[..., 2]
+        its.append(float(it.sum()))
+        trk.append(float((it >= 1).sum()))
+    ctx.close()
+    it_pair, trk_pair = float(np.mean(its)), float(np.mean(trk))
+    lanes = 1600.0 * (LK_VALU_PER_ELEM_A * trk_pair + LK_VALU_PER_ELEM_ITER * it_pair)
+    return dict(iterations_per_pair=round(it_pair, 1), iterations_per_point=round(it_pair / n, 3),
+                tracked_level_points_per_pair=round(trk_pair, 1), valu_lane_instr_per_pair=lanes, levels=nl)
+
+
 def open_ctx(D: Dist, w: int, h: int, batch: int, **params):
     """One context on this rank's GPU (LOCAL_RANK).  A rank whose device is not visible is an
     error (exit 3) unless --rehearse is given: then it shares device 0, and the JSON line's n_gpus
@@ -379,6 +422,7 @@ def main():
     ap.add_argument("--no-4k", action="store_true", help="skip the whole-path 4K leg (config C2)")
     ap.add_argument("--rehearse", action="store_true",
                     help="allow more ranks than visible GPUs (they share device 0; n_gpus counts distinct devices)")
+    ap.add_argument("--no-lk-roofline", action="store_true", help="skip the LK iteration census (profiling runs)")
     ap.add_argument("--probe-ranks", action="store_true", help="launch plumbing only: ranks report over gloo, no GPU")
     args = ap.parse_args()
     global REHEARSE
@@ -520,6 +564,26 @@ def main():
         live = live_leg(D.local_rank, w, h, threads, with_cpu=not args.no_cpu)
 
     lk_share = stages["lk"] / stages["total"] if stages["total"] > 0 else None
+    # VALU roofline of the dominant stage (LK): algorithmic wave-instructions of the
+    # step's B pairs over the LK stage's HIP-event time, against the chip's VALU issue rate
+    lk_roof = None
+    if not args.only_roofline and not args.no_lk_roofline and stages.get("lk", 0) > 0:
+        wk = lk_work(ctx.device, w, h, ps, uniq)
+        alg_wave = wk["valu_lane_instr_per_pair"] * B / 64.0
+        ach = alg_wave / (stages["lk"] * 1e-3)
+        lk_roof = dict(bound="valu", unit="wave-instr/s", achieved=round(ach, 1), peak=VALU_PEAK_WAVE_INSTR,
+                       frac=round(ach / VALU_PEAK_WAVE_INSTR, 4), stage_ms=stages["lk"],
+                       algorithmic_wave_instr_per_step=round(alg_wave, 1), per_element=dict(
+                           iteration=LK_VALU_PER_ELEM_ITER, gradient_sums=LK_VALU_PER_ELEM_A),
+                       workload=f"{B} pairs {w}x{h}, pixel_step {ps}, {wk['levels']} levels", **{
+                           k: v for k, v in wk.items() if k not in ("valu_lane_instr_per_pair", "levels")})
+        pmc = os.path.join(ROOT, "profiles", "pmc_lk.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                pj = json.load(f)
+            if pj.get("config") == f"{w}x{h}x{B}_ps{ps}":
+                lk_roof["executed_wave_instr_per_step"] = pj.get("sq_insts_valu_per_step")
+                lk_roof["executed_over_algorithmic"] = round(pj["sq_insts_valu_per_step"] / alg_wave, 3)
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -545,9 +609,11 @@ def main():
         "devices": devs["devices"],
         "build": mdx._lib.build_info(),
         "stage_ms_per_step": stages,
-        "dominant_kernel": {"name": "k_lk", "share_of_step": round(lk_share, 4) if lk_share else None,
+        "dominant_kernel": {"name": "k_lk_class + k_lk_A + k_lk_iter (LK stage)",
+                            "share_of_step": round(lk_share, 4) if lk_share else None,
                             "bound": "valu/lds (exact-order float chains), not hbm",
-                            "points_per_s": round(px_all / (w * h) * mdx.grid_count(w, h, ps) / el_max, 1)},
+                            "points_per_s": round(px_all / (w * h) * mdx.grid_count(w, h, ps) / el_max, 1),
+                            "roofline": lk_roof},
         "num_vectors_pair0": int(num[0]),
         "full_path_4k": full4k,
         "live_path": live,

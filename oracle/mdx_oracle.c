@@ -461,6 +461,36 @@ static inline uint32_t rng_next(uint64_t* state)
     return (uint32_t)*state;
 }
 
+/* The two readings of JacobiSVDImpl_ under CV_SSE2.  VBLAS<double>::givens (the Vt
+ * rotations) computes every element exactly as the scalar loop, so it needs no restatement.  If
+ * the column dot product and the rotated columns' norms went through VBLAS<double>::dot / givensx,
+ * they would accumulate in two-lane SSE2 partials: dot over 4-element steps into two __m128d
+ * accumulators, result ((s0 + s1)[0] + (s0 + s1)[1]) then a scalar tail; givensx over 2-element
+ * steps, norms (lane 0 + lane 1) then a scalar tail.  g_svd_vblas = 1 selects that reading;
+ * 0 (default, what the GPU restates) the scalar loops. */
+static int g_svd_vblas = 0;
+void ora_set_svd_vblas(int on) { g_svd_vblas = on != 0; }
+
+static double vblas_dot(const double* a, const double* b, int n)
+{
+    if (n < 4) {
+        double p = 0;
+        for (int k = 0; k < n; k++) p += a[k] * b[k];
+        return p;
+    }
+    double s00 = 0, s01 = 0, s10 = 0, s11 = 0;
+    int k = 0;
+    for (; k <= n - 4; k += 4) {
+        s00 = s00 + a[k] * b[k];
+        s01 = s01 + a[k + 1] * b[k + 1];
+        s10 = s10 + a[k + 2] * b[k + 2];
+        s11 = s11 + a[k + 3] * b[k + 3];
+    }
+    double p = (s00 + s10) + (s01 + s11);
+    for (; k < n; k++) p += a[k] * b[k];
+    return p;
+}
+
 /* lapack.cpp JacobiSVDImpl_<double>(At, W, Vt, m, n, n1=n, minval=DBL_MIN, eps=10*DBL_EPSILON).
  * At: n rows of length m (rows are columns of A); Vt: n x n. */
 static void jacobi_svd(double* At, int m, int n, double* Wout, double* Vt)
@@ -481,7 +511,9 @@ static void jacobi_svd(double* At, int m, int n, double* Wout, double* Vt)
             for (j = i + 1; j < n; j++) {
                 double *Ai = At + i * m, *Aj = At + j * m;
                 double a = W[i], p = 0, b = W[j];
-                for (k = 0; k < m; k++) p += Ai[k] * Aj[k];
+                if (g_svd_vblas) p = vblas_dot(Ai, Aj, m);
+                else
+                    for (k = 0; k < m; k++) p += Ai[k] * Aj[k];
                 if (fabs(p) <= eps * sqrt(a * b)) continue;
                 p *= 2;
                 double beta = a - b, gamma = ora_hypot(p, beta);
@@ -494,7 +526,20 @@ static void jacobi_svd(double* At, int m, int n, double* Wout, double* Vt)
                     s = p / (gamma * c * 2);
                 }
                 a = b = 0;
-                for (k = 0; k < m; k++) {
+                k = 0;
+                if (g_svd_vblas) {   /* givensx: two lanes, then lane 0 + lane 1 */
+                    double a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+                    for (; k <= m - 2; k += 2) {
+                        double t00 = Ai[k] * c + Aj[k] * s, t01 = Ai[k + 1] * c + Aj[k + 1] * s;
+                        double t10 = Aj[k] * c - Ai[k] * s, t11 = Aj[k + 1] * c - Ai[k + 1] * s;
+                        Ai[k] = t00; Ai[k + 1] = t01; Aj[k] = t10; Aj[k + 1] = t11;
+                        a0 = a0 + t00 * t00; a1 = a1 + t01 * t01;
+                        b0 = b0 + t10 * t10; b1 = b1 + t11 * t11;
+                    }
+                    a = a0 + a1;
+                    b = b0 + b1;
+                }
+                for (; k < m; k++) {
                     double t0 = c * Ai[k] + s * Aj[k];
                     double t1 = -s * Ai[k] + c * Aj[k];
                     Ai[k] = t0; Aj[k] = t1;

@@ -69,6 +69,8 @@ void ora_lk(const ora_pyramid* prev, const ora_pyramid* next, int max_level,
             const float* prev_pts, float* next_pts, uint8_t* status, int npts,
             const ora_params* prm, int nthreads);
 
+/* 1: JacobiSVDImpl_ with SSE2 VBLAS dot/givensx partial sums (see mdx_oracle.c); 0: scalar (default) */
+void ora_set_svd_vblas(int on);
 void ora_get_perspective_transform(const float src[8], const float dst[8], double M[9]);
 int  ora_invert3x3(const double M[9], double Minv[9]);
 void ora_warp_perspective(const uint8_t* src, int w, int h, int sstride, const double M[9],

@@ -61,6 +61,8 @@ def lib():
         L.ora_lk.argtypes = [C.POINTER(OraPyramid), C.POINTER(OraPyramid), C.c_int, f32p, f32p, u8p,
                              C.c_int, C.POINTER(OraParams), C.c_int]
         L.ora_get_perspective_transform.argtypes = [f32p, f32p, f64p]
+        L.ora_set_svd_vblas.argtypes = [C.c_int]
+        L.ora_set_svd_vblas.restype = None
         L.ora_invert3x3.argtypes = [f64p, f64p]
         L.ora_invert3x3.restype = C.c_int
         L.ora_warp_perspective.argtypes = [u8p, C.c_int, C.c_int, C.c_int, f64p, u8p, C.c_int, C.c_int]
@@ -154,6 +156,12 @@ def get_perspective_transform(src4: np.ndarray, dst4: np.ndarray) -> np.ndarray:
     M = np.zeros(9)
     lib().ora_get_perspective_transform(_p(s, C.c_float), _p(d, C.c_float), _p(M, C.c_double))
     return M.reshape(3, 3)
+
+
+def set_svd_vblas(on: bool) -> None:
+    """Select the JacobiSVDImpl_ reading: False (default) scalar loops, True SSE2 VBLAS
+    dot / givensx partial sums."""
+    lib().ora_set_svd_vblas(1 if on else 0)
 
 
 def invert3x3(M: np.ndarray) -> np.ndarray:

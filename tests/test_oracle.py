@@ -203,3 +203,32 @@ def test_grid_order_is_x_major(oracle):
     pts = npr.grid_points(25, 17, 10)
     assert oracle.grid_count(25, 17, 10) == len(pts) == 3 * 2
     assert pts[:3].tolist() == [[0, 0], [0, 10], [10, 0]]
+
+
+def test_svd_vblas_reading_sensitivity(oracle):
+    """OpenCV 2.4's JacobiSVDImpl_ under CV_SSE2 may route the column dot products and norms
+    through VBLAS<double>::dot / givensx (two-lane partial sums).  Both readings are valid SVD
+    solves; this pins how far apart they leave getPerspectiveTransform: the
+    matrices agree to 1e-9 relative, and the share of bit-different entries is recorded."""
+    rng = np.random.default_rng(11)
+    diff = total = 0
+    worst = 0.0
+    try:
+        for t in range(400):
+            if t % 4 == 0:   # the reference's usual case: four points of column x = 0 (collinear)
+                src = np.array([[0, 10 * i] for i in range(4)], np.float32)
+            else:
+                src = rng.uniform(0, 1920, (4, 2)).astype(np.float32)
+            dst = (src + rng.normal(0, 3, (4, 2))).astype(np.float32)
+            oracle.set_svd_vblas(False)
+            M0 = oracle.get_perspective_transform(src, dst)
+            oracle.set_svd_vblas(True)
+            M1 = oracle.get_perspective_transform(src, dst)
+            total += 9
+            diff += int((M0.view(np.uint64) != M1.view(np.uint64)).sum())
+            scale = np.maximum(np.abs(M0), 1e-300)
+            worst = max(worst, float(np.max(np.abs(M1 - M0) / np.maximum(scale, 1.0))))
+    finally:
+        oracle.set_svd_vblas(False)
+    print(f"VBLAS reading: {diff} of {total} H entries bit-different, worst relative {worst:.3g}")
+    assert worst < 1e-9
