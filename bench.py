@@ -248,86 +248,106 @@ def probe_ranks(D: Dist) -> None:
 
 
 def main_c4(args, D: Dist, threads: int):
-    """Config C4: one 8K RGB pair row-tiled over the ranks.  `--bands K` splits the frame
+    """Config C4: 8K RGB pairs row-tiled over the ranks.  `--bands K` splits the frame
     into K bands dealt round-robin to the ranks (K > ranks rehearses a K-GPU split on fewer GPUs).
-    Per step: each rank runs its bands' flow, the 96-byte band records are all-gathered (gloo,
-    host side), then each rank fits (identically) and writes its bands' mask rows.  Strong scaling:
-    the frame is fixed, `value` = frame pixels / max-over-ranks step time."""
+    Per frame: each rank runs its bands' flow, the 96-byte band records are all-gathered (gloo,
+    host side), then each rank fits (identically) and writes its bands' mask rows.
+    `--inflight F` (default 2) keeps F consecutive frames in flight per GPU, each on its own context
+    and HIP stream: one frame's band LK (a few thousand points, latency-bound, half the chip idle)
+    overlaps the next frame's front end and LK.  A step is F frames; strong scaling: the frames are
+    fixed, `value` = F x frame pixels / max-over-ranks step time."""
     from motion_detection_amd import rowtile
     w, h = CONFIGS[args.config] if args.config != "1080p" else CONFIGS["8k"]
     ps, fmt = 10, mdx.FMT_RGB8
     K = args.bands or D.world
+    F = max(1, args.inflight)
     mine = list(range(D.rank, K, D.world))
     per_rank = -(-K // D.world)
     a, b, _ = mdx.synth_pair(SEED0 + 4, w, h, 3, threads)       # every rank: the same frame pair
-    ctx = open_ctx(D, w, h, 1, pixel_step=ps, min_vector_size=1.0)
-    devs = gather_devices(D, ctx)
+    ctxs = [open_ctx(D, w, h, 1, pixel_step=ps, min_vector_size=1.0) for _ in range(F)]
+    devs = gather_devices(D, ctxs[0])
     n = mdx.grid_count(w, h, ps)
-    d = {k: ctx.dev_alloc(sz) for k, sz in dict(i1=a.nbytes, i2=b.nbytes, np=n * 8, st=n, cand=per_rank * 96,
-                                               cands=K * 96, mask=w * h, num=4).items()}
-    ctx.h2d(d["i1"], a)
-    ctx.h2d(d["i2"], b)
+    bufs = []
+    for c in ctxs:
+        d = {k: c.dev_alloc(sz) for k, sz in dict(i1=a.nbytes, i2=b.nbytes, np=n * 8, st=n, cand=per_rank * 96,
+                                                 cands=K * 96, mask=w * h, num=4).items()}
+        c.h2d(d["i1"], a)
+        c.h2d(d["i2"], b)
+        bufs.append(d)
     rows = [rowtile.band_rows(h, K, k) for k in range(K)]
     pad = bytes(96)
     t_ph = {"flow": 0.0, "exchange": 0.0, "fit_warp": 0.0}
 
-    def step(timed=False):
-        t0 = time.perf_counter()
-        for j, k in enumerate(mine):
-            ctx.band_flow_dev(d["i1"], d["i2"], w, h, w * 3, fmt, *rows[k], d["np"], d["st"], d["cand"] + 96 * j)
+    def exchange(c, d):
         rec = np.empty(per_rank * 96, np.uint8)
-        ctx.d2h(rec, d["cand"])                                  # synchronous: the flow is done
-        t1 = time.perf_counter()
+        c.d2h(rec, d["cand"])                                    # synchronous: this frame's flow is done
         local = rec.tobytes()[:96 * len(mine)] + pad * (per_rank - len(mine))
         parts = D.allgather_bytes(local)
         allrec = bytearray(K * 96)
         for r, part in enumerate(parts):                         # rank r holds bands r, r + world, ...
             for j, k in enumerate(range(r, K, D.world)):
                 allrec[96 * k:96 * (k + 1)] = part[96 * j:96 * (j + 1)]
-        ctx.h2d(d["cands"], np.frombuffer(bytes(allrec), np.uint8))
-        t2 = time.perf_counter()
-        for k in mine:
-            ctx.band_fit_warp_dev(K, d["cands"], *rows[k], d["mask"] + rows[k][0] * w, 0, d["num"])
-        ctx.sync()
+        c.h2d(d["cands"], np.frombuffer(bytes(allrec), np.uint8))
+
+    def step(timed=False):
+        t0 = time.perf_counter()
+        for c, d in zip(ctxs, bufs):                             # every in-flight frame's flow, async
+            for j, k in enumerate(mine):
+                c.band_flow_dev(d["i1"], d["i2"], w, h, w * 3, fmt, *rows[k], d["np"], d["st"], d["cand"] + 96 * j)
+        t1 = time.perf_counter()
+        tx = 0.0
+        for c, d in zip(ctxs, bufs):                             # then, frame by frame: records, fit, warp
+            e0 = time.perf_counter()
+            exchange(c, d)
+            tx += time.perf_counter() - e0
+            for k in mine:
+                c.band_fit_warp_dev(K, d["cands"], *rows[k], d["mask"] + rows[k][0] * w, 0, d["num"])
+        for c in ctxs:
+            c.sync()
         t3 = time.perf_counter()
         if timed:
             t_ph["flow"] += t1 - t0
-            t_ph["exchange"] += t2 - t1
-            t_ph["fit_warp"] += t3 - t2
+            t_ph["exchange"] += tx
+            t_ph["fit_warp"] += t3 - t1 - tx
 
     for _ in range(args.warmup):
         step()
     D.barrier()
-    ctx.device_sync()
+    for c in ctxs:
+        c.device_sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(timed=True)
-    ctx.device_sync()
+    for c in ctxs:
+        c.device_sync()
     D.barrier()
     el = time.perf_counter() - t0
     el_max = D.max(el)
     num = np.empty(1, np.int32)
-    ctx.d2h(num, d["num"])
-    # one band alone (K bands on K GPUs: each GPU's share), timed here for the rehearsal case
-    band_ms, band_stages = None, None
+    ctxs[0].d2h(num, bufs[0]["num"])
+    # one band alone per in-flight frame (K bands on K GPUs: each GPU's share), timed here for the
+    # rehearsal case: F frames of band mine[0], amortised per frame
+    band_ms = None
     if K > D.world and mine:
         k = mine[0]
         reps = max(2, args.steps)
-        ctx.device_sync()
-        ctx.enable_timing(True)
+        for c in ctxs:
+            c.device_sync()
         tb = time.perf_counter()
         for _ in range(reps):
-            ctx.band_flow_dev(d["i1"], d["i2"], w, h, w * 3, fmt, *rows[k], d["np"], d["st"], d["cand"])
-            ctx.band_fit_warp_dev(K, d["cands"], *rows[k], d["mask"] + rows[k][0] * w, 0, d["num"])
-        ctx.device_sync()
-        band_ms = (time.perf_counter() - tb) / reps * 1e3
-        st = ctx.stage_ms()
-        band_stages = {kk: round(v / max(st["calls"], 1), 4) for kk, v in st.items() if kk != "calls"}
-    for p in d.values():
-        ctx.dev_free(p)
+            for c, d in zip(ctxs, bufs):
+                c.band_flow_dev(d["i1"], d["i2"], w, h, w * 3, fmt, *rows[k], d["np"], d["st"], d["cand"])
+            for c, d in zip(ctxs, bufs):
+                c.band_fit_warp_dev(K, d["cands"], *rows[k], d["mask"] + rows[k][0] * w, 0, d["num"])
+        for c in ctxs:
+            c.device_sync()
+        band_ms = (time.perf_counter() - tb) / (reps * F) * 1e3
+    for c, d in zip(ctxs, bufs):
+        for p in d.values():
+            c.dev_free(p)
     out = {
         "metric": METRIC,
-        "value": round(args.steps * w * h / el_max / 1e6, 2),
+        "value": round(args.steps * F * w * h / el_max / 1e6, 2),
         "unit": "Mpixels/s",
         "n_gpus": devs["n_gpus"],
         "ranks": devs["ranks"],
@@ -335,26 +355,27 @@ def main_c4(args, D: Dist, threads: int):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(el_max / args.steps * 1e3, 3),
+        "ms_per_frame": round(el_max / (args.steps * F) * 1e3, 3),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (mdx_synth_pair, rgb8)",
-        "config": {"workload": f"C4: one {w}x{h} RGB pair per step, row-tiled into {K} bands over "
+        "config": {"workload": f"C4: {w}x{h} RGB pairs, {F} in flight per GPU, each row-tiled into {K} bands over "
                                f"{D.world} rank(s); per band LK + classify, one 96-B record all-gather, "
                                f"identical fit on every rank, band warp+absdiff+threshold",
-                   "frame": f"{w}x{h}", "pixel_step": ps, "bands": K, "bands_per_rank": per_rank,
+                   "frame": f"{w}x{h}", "pixel_step": ps, "bands": K, "bands_per_rank": per_rank, "inflight": F,
                    "parallelism": f"row bands, {D.world} rank(s), record exchange over gloo (host)"},
         "phase_ms_per_step_rank0": {k: round(v / args.steps * 1e3, 3) for k, v in t_ph.items()},
         "one_band_ms": round(band_ms, 3) if band_ms else None,
-        "one_band_stage_ms": band_stages,
         "num_vectors": int(num[0]),
         "roofline": None,
         "cpu_baseline": None,
     }
     if D.rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     D.close()
 
 
@@ -418,6 +439,7 @@ def main():
     ap.add_argument("--workload", default="c1", choices=["c1", "c4"],
                     help="c1: batched 1080p stream shards (the metric's config); c4: 8K RGB row-tiled")
     ap.add_argument("--bands", type=int, default=0, help="c4: row bands (default: one per rank)")
+    ap.add_argument("--inflight", type=int, default=2, help="c4: frames in flight per GPU (one context each)")
     ap.add_argument("--no-live", action="store_true", help="skip the node's live trajectory + RANSAC leg")
     ap.add_argument("--no-4k", action="store_true", help="skip the whole-path 4K leg (config C2)")
     ap.add_argument("--rehearse", action="store_true",
