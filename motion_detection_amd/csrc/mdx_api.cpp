@@ -515,18 +515,23 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
     PairFit* fits = c->fits.as<PairFit>();
 
     mark(c, 0);
-    HIP_OR_RETURN(c, launch_gray_pad(s, batch, d_img1, d_img2, w, h, stride, (long long)frame_stride, fmt, pyr1, pyr2, g));
-    mark(c, 1);
     // The class planes and A sums need only the first frames' pyramids: build those first and let
-    // the aux stream start on them while the second frames' pyramids are built
+    // the aux stream start on them while the second frames' pyramids are built.  Stage "gray_pad"
+    // = gray + pad + level 1 of the first frames (k_front), "pyrdown" = the rest of the pyramids.
     hipEvent_t prev_ready = nullptr;
+    const long long fs = (long long)frame_stride;
     if (c->aux && c->lk_impl == 2) {
-        for (int l = 1; l < g.nlev; l++) HIP_OR_RETURN(c, launch_pyrdown(s, batch, pyr1, pyr2, g, l, 1));
+        HIP_OR_RETURN(c, launch_front(s, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g, 1));
+        mark(c, 1);
+        HIP_OR_RETURN(c, launch_pyr_levels(s, batch, pyr1, pyr2, g, 1));
         HIP_OR_RETURN(c, hipEventRecord(c->lkev[kMaxLevels + 1], s));
         prev_ready = c->lkev[kMaxLevels + 1];
-        for (int l = 1; l < g.nlev; l++) HIP_OR_RETURN(c, launch_pyrdown(s, batch, pyr1, pyr2, g, l, 2));
+        HIP_OR_RETURN(c, launch_front(s, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g, 2));
+        HIP_OR_RETURN(c, launch_pyr_levels(s, batch, pyr1, pyr2, g, 2));
     } else {
-        for (int l = 1; l < g.nlev; l++) HIP_OR_RETURN(c, launch_pyrdown(s, batch, pyr1, pyr2, g, l));
+        HIP_OR_RETURN(c, launch_front(s, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g));
+        mark(c, 1);
+        HIP_OR_RETURN(c, launch_pyr_levels(s, batch, pyr1, pyr2, g));
     }
     mark(c, 2);
     // Scharr derivatives feed only the LK.  The class-plane LK launches them itself, on its
@@ -687,8 +692,8 @@ extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int n
     uint8_t* pyr1 = c->pyr1.as<uint8_t>();
     uint8_t* pyr2 = c->pyr2.as<uint8_t>();
     uint32_t* der = c->der.as<uint32_t>();
-    HIP_OR_RETURN(c, launch_gray_pad(s, npairs, din, din + fbytes, w, h, stride, (long long)fbytes, fmt, pyr1, pyr2, g));
-    for (int l = 1; l < g.nlev; l++) HIP_OR_RETURN(c, launch_pyrdown(s, npairs, pyr1, pyr2, g, l));
+    HIP_OR_RETURN(c, launch_front(s, npairs, din, din + fbytes, w, h, stride, (long long)fbytes, fmt, pyr1, pyr2, g));
+    HIP_OR_RETURN(c, launch_pyr_levels(s, npairs, pyr1, pyr2, g));
     for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, npairs, pyr1, der, g, l));
     float* cur = c->tcur.as<float>();
     float* tr = c->ttraj.as<float>();

@@ -111,8 +111,12 @@ struct LkArgs {
 hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const uint8_t* in2, int w, int h,
                            int stride, long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2,
                            const Geometry& g, int fsel = 0);
-hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level,
-                          int fsel = 0);
+// gray + pad of level 0 and pyrDown to level 1 in one pass (k_front; launch_gray_pad when nlev == 1);
+// launch_pyr_levels then builds levels 2 .. nlev-1 (k_front in level mode, one launch per level)
+hipError_t launch_front(hipStream_t s, int batch, const uint8_t* in1, const uint8_t* in2, int w, int h, int stride,
+                        long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g,
+                        int fsel = 0);
+hipError_t launch_pyr_levels(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int fsel = 0);
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level);
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
 // Trajectory subspace RANSAC (fitSubspace): mean-subtracted data, nhyp hypotheses of d columns

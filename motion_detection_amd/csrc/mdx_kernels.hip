@@ -5,8 +5,9 @@
 // of the OpenCV 2.4 routine the reference calls, bit for bit (integer stages exactly; float
 // and double stages in the same evaluation order, compiled with -ffp-contract=off so no
 // expression is fused into an FMA).  Stage map:
-//   A1      k_gray_pad       cvtColor(BGR2GRAY) on rgb8 + level-0 REFLECT_101 padding
-//   A3/A4   k_pyrdown        pyrDown + REFLECT_101 padding, both frames of every pair
+//   A1-A4   k_front          cvtColor(BGR2GRAY) + level-0 REFLECT_101 padding + pyrDown to level 1
+//                            in one pass; in level mode pyrDown L -> L+1 for the coarser levels
+//   A1      k_gray_pad       gray + level-0 padding alone (single-level pyramids)
 //   A3      k_scharr         calcSharrDeriv + CONSTANT-0 padding (prev frame)
 //   A5      k_lk             calcOpticalFlowPyrLK (LKTrackerInvoker, SSE2 summation order)
 //   A6/A7   k_classify/k_fit Vec4d classification, first-4 getPerspectiveTransform, invert
@@ -105,70 +106,294 @@ __global__ __launch_bounds__(256) void k_gray_pad(const uint8_t* __restrict__ in
     if (two) *reinterpret_cast<uint4*>(row + 16 * (c + 1)) = make_uint4(o1[0], o1[1], o1[2], o1[3]);
 }
 
-// ------------------------------------------------------------------ A3/A4: pyrDown
+// ------------------------------------------------------------------ A1 + A3/A4: k_front
+// buildOpticalFlowPyramid's images (lkpyramid.cpp, called at optical_flow_calculator.cpp:71):
 // pyramids.cpp pyrDown_<FixPtCast<uchar,8>>: dst(x,y) = (sum_ij k_i k_j src(r101(2y+i-2),
-// r101(2x+j-2)) + 128) >> 8, k = [1 4 6 4 1], on the source ROI's own size.  The source level
-// already carries its REFLECT_101 border (>= 2 px), so its taps are read straight from the
-// padded buffer; the destination border is the reflect-101 image of the destination core
-// (copyMakeBorder ... BORDER_REFLECT_101|BORDER_ISOLATED), computed in place.
-// Per thread 4 destination pixels; each source row segment is one 16-B load and the 5-tap row
-// filter is two chained v_dot4_u32_u8 per output.
-__device__ __forceinline__ uint32_t pyr_px(const uint8_t* src, int sp, int cx, int cy)
+// r101(2x+j-2)) + 128) >> 8, k = [1 4 6 4 1], on the source ROI's own size; every level carries a
+// 40-px REFLECT_101 border of its own core (copyMakeBorder ... BORDER_REFLECT_101|BORDER_ISOLATED).
+//
+// Frame mode (MODE 0/1): gray + level-0 padding + level 1 in one pass.  A workgroup owns RB level-1
+// core rows [Y0, Y0+RB) and the level-0 core rows [2 Y0, 2 Y0 + 2 RB):
+//   1  stage level-0 padded rows 2 Y0 - 2 .. 2 Y0 + 2 RB (reflect-101 in both directions, gray of
+//      rgb8 on the fly) in LDS: interior 16-B chunks by vector loads, K per thread in flight, the
+//      border bytes one per lane;
+//   2  write the band's level-0 rows, and every border row that mirrors one of them, from LDS;
+//   3a level-1 core rows into an LDS row buffer: a thread owns 4 level-1 columns and walks down
+//      the band, each staged row's horizontal 5-tap sums (two chained v_dot4_u32_u8 per pixel)
+//      computed once and reused by the up to three level-1 rows whose vertical window covers it;
+//   3a' the row buffer's reflect-101 column borders, one byte per lane;
+//   3b level-1 padded rows (and mirrored border rows) out, 16 B per lane.
+// Level 0 thus crosses HBM once (written) instead of three times (written, read back by a
+// separate pyrDown); source halo rows are shared with the neighbouring band through L2
+// (consecutive bands go to the same XCD).  Level mode (MODE 2) runs the same band schedule from
+// an already padded level to the next (phase 1 = plain 16-B copies of the padded source rows, no
+// phase 2).  Measured at 1080p x 32, one frame side (scripts/micro/front_bench.hip): levels 0-1
+// 44 us (3.7 TB/s of 162 MB) and levels 2-4 32 us, against 107 + 42 us for the earlier
+// k_gray_pad + per-level pyrDown kernels.  Per-pixel reflect-101 gathers in the hot loops cost
+// ~2-5 us per workgroup (measured): borders are built byte-per-lane from data already in LDS.
+struct FrontArgs {
+    const uint8_t* in1;
+    const uint8_t* in2;
+    int w, h, stride, fmt, fsel, nbands, nz;
+    long long frame_stride, img_bytes;
+    uint8_t* pyr1;
+    uint8_t* pyr2;
+    Level L0, L1;
+    int nchunk0;     // last 16-B chunk of a level-0 row (chunk 0 is margin)
+    int nchunk1_16;  // last 16-B chunk of a level-1 row (chunk 0 is margin)
+    int aligned;     // every source row starts 4-B aligned (interior chunks take vector loads)
+    int lp;          // LDS bytes per staged level-0 row (16 * (nchunk0 + 1))
+    int lp1;         // LDS bytes per level-1 row of the row buffer (16 * (nchunk1_16 + 1))
+};
+
+// borderInterpolate(p, len, BORDER_REFLECT_101) for -len < p < 2 len - 1 (one fold), branch-free.
+// k_front only runs when level 1 exists, i.e. w, h >= 81 and the level-1 sizes are >= 41, so
+// every index it folds (at most 40 outside a row or column range) needs at most one fold.
+__device__ __forceinline__ int r101s(int p, int len)
 {
-    const uint8_t* s0 = src + (long long)(2 * cy - 2) * sp + (2 * cx - 2);
-    int acc = 0;
-#pragma unroll
-    for (int i = 0; i < 5; i++) {
-        const uint8_t* r = s0 + (long long)i * sp;
-        const int hrow = r[2] * 6 + (r[1] + r[3]) * 4 + r[0] + r[4];
-        acc += hrow * (i == 2 ? 6 : (i == 1 || i == 3) ? 4 : 1);
-    }
-    return (uint32_t)((acc + 128) >> 8);
+    const int q = p < 0 ? -p : p;
+    return q >= len ? 2 * len - 2 - q : q;
 }
 
-__global__ __launch_bounds__(256) void k_pyrdown(uint8_t* __restrict__ pyr1, uint8_t* __restrict__ pyr2,
-                                                 long long img_bytes, Level S, Level D, int nchunk, int fsel)
+__device__ __forceinline__ int fdiv(int a, int b, float rb)
 {
-    // 4 destination pixels (one dword) per thread
-    const int which = fsel ? fsel - 1 : blockIdx.z & 1, pair = fsel ? blockIdx.z : blockIdx.z >> 1;
-    const int c = blockIdx.x * blockDim.x + threadIdx.x + 6;         // dword chunks 0..5 are margin
-    const int py = blockIdx.y - kPad;
-    if (c > nchunk) return;
-    uint8_t* slab = (which ? pyr2 : pyr1) + (long long)pair * img_bytes;
-    const uint8_t* src = slab + S.img_off + S.core();
-    const int px0 = 4 * c - kXOff;
-    const int cy = r101(py, D.h);
-    uint32_t o = 0;
-    if (px0 >= 0 && px0 + 4 <= D.w) {
-        // source columns 2*px0-4 .. 2*px0+11: one 16-B load per row (4-B aligned)
-        const uint8_t* s0 = src + (long long)(2 * cy - 2) * S.pitch + (2 * px0 - 4);
-        uint32_t acc[4] = {0, 0, 0, 0};
+    // a / b for 0 <= a < 2^20 (b > 0): float estimate, corrected
+    int q = (int)((float)a * rb);
+    if (q * b > a) q--;
+    else if ((q + 1) * b <= a) q++;
+    return q;
+}
+
+// MODE 0: mono8 frames, 1: rgb8/bgr8 frames (gray + pad + level 1, as above); MODE 2: one
+// pyramid level L -> L+1 (a.L0 = source level, already padded in the slab, a.L1 = destination):
+// the staged rows are plain 16-B copies of the padded source rows and phase 2 is skipped.
+template <int RB, int MODE, int KM = 8>
+__global__ __launch_bounds__(256) void k_front(FrontArgs a)
+{
+    constexpr bool COLOR = MODE == 1, FRAME = MODE != 2;
+    constexpr int NR = 2 * RB + 3, K = COLOR ? 2 : KM, VW = COLOR ? 12 : 4, MAXOUT0 = 2 * RB + 80, MAXOUT1 = RB + 80;
+    extern __shared__ uint32_t front_lds[];
+    __shared__ int out0[MAXOUT0], out1[MAXOUT1], nout[2];
+    uint8_t* lds = reinterpret_cast<uint8_t*>(front_lds);
+    const int tid = threadIdx.x;
+
+    // XCD-aware order: consecutive bands of a frame go to the same XCD (8 dispatch round-robin)
+    const int nb = gridDim.x;
+    int task = blockIdx.x;
+    if ((nb & 7) == 0) task = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
+    const int band = task % a.nbands, z = task / a.nbands;
+    const int which = a.fsel ? a.fsel - 1 : z & 1, pair = a.fsel ? z : z >> 1;
+    const int w = a.w, h = a.h, w1 = a.L1.w, h1 = a.L1.h;
+    const int Y0 = band * RB, e1 = min(Y0 + RB, h1), r0 = 2 * Y0, e0 = min(2 * Y0 + 2 * RB, h);
+    const int fmt = a.fmt;
+    const uint8_t* src = (which ? a.in2 : a.in1) + (long long)pair * a.frame_stride;
+    uint8_t* slab = (which ? a.pyr2 : a.pyr1) + (long long)pair * a.img_bytes;
+
+    // rows this band writes: level 0 padded rows whose core row is in [r0, e0), level 1 in [Y0, e1)
+    if (tid < 2) nout[tid] = 0;
+    __syncthreads();
+    if (FRAME && tid < 80) {
+        const int py = tid < 40 ? tid - 40 : h + tid - 40;
+        const int r = r101s(py, h);
+        if (r >= r0 && r < e0) out0[atomicAdd(&nout[0], 1)] = py;
+    } else if (tid >= 128 && tid < 208) {
+        const int t = tid - 128;
+        const int py = t < 40 ? t - 40 : h1 + t - 40;
+        const int r = r101s(py, h1);
+        if (r >= Y0 && r < e1) out1[atomicAdd(&nout[1], 1)] = py;
+    }
+    __syncthreads();
+    const int nb0 = nout[0], nb1 = nout[1];
+    __syncthreads();
+    if (FRAME && tid < e0 - r0) out0[nb0 + tid] = r0 + tid;
+    if (tid >= 128 && tid - 128 < e1 - Y0) out1[nb1 + tid - 128] = Y0 + tid - 128;
+
+    // phase 1: level-0 padded rows r0-2 .. r0+2RB into LDS (chunks 1 .. nchunk0).  Interior chunks
+    // [cA, cB] (inside the source row, every row 4-B aligned per the host) take plain 16-B (mono8)
+    // or 48-B (rgb8/bgr8) loads, K per thread in flight; the few border chunks go through the
+    // per-pixel reflect-101 path in a loop of their own.
+    const int nc0 = a.nchunk0;
+    if constexpr (!FRAME) {
+        // padded source rows r0-2 .. r0+2RB of level a.L0, chunks 1 .. nc0, K loads in flight
+        const uint8_t* lvl = slab + a.L0.img_off + (long long)kPad * a.L0.pitch;
+        const float rc = 1.f / (float)nc0;
+        const int n1 = NR * nc0;
+        for (int base = 0; base < n1; base += 256 * K) {
+            uint4 v[K];
 #pragma unroll
-        for (int i = 0; i < 5; i++) {
-            const u4a4k a = *reinterpret_cast<const u4a4k*>(s0 + (long long)i * S.pitch);
-            const uint32_t wd[4] = {a.x, a.y, a.z, a.w};
-            const uint32_t ki = i == 2 ? 6u : (i == 1 || i == 3) ? 4u : 1u;
+            for (int k = 0; k < K; k++) {
+                const int item = base + k * 256 + tid;
+                if (item < n1) {
+                    const int i = fdiv(item, nc0, rc), c = 1 + item - i * nc0;
+                    v[k] = *reinterpret_cast<const uint4*>(lvl + (long long)(r0 - 2 + i) * a.L0.pitch + 16 * c);
+                }
+            }
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                // taps at bytes 2j+2 .. 2j+6 of the segment
-                const int b0 = 2 * j + 2, q = b0 >> 2;
-                const uint32_t lo = (b0 & 3) ? __builtin_amdgcn_alignbit(wd[q + 1], wd[q], 16) : wd[q];
-                const uint32_t hi = (b0 & 3) ? (wd[q + 1] >> 16) : wd[q + 1];
-                const uint32_t hrow = __builtin_amdgcn_udot4(hi, 1u, __builtin_amdgcn_udot4(lo, 0x04060401u, 0u, false), false);
-                acc[j] += hrow * ki;
+            for (int k = 0; k < K; k++) {
+                const int item = base + k * 256 + tid;
+                if (item >= n1) continue;
+                const int i = fdiv(item, nc0, rc), c = 1 + item - i * nc0;
+                *reinterpret_cast<uint4*>(lds + i * a.lp + 16 * c) = v[k];
             }
         }
-        o = ((acc[0] + 128) >> 8) | (((acc[1] + 128) >> 8) << 8) | (((acc[2] + 128) >> 8) << 16) |
-            (((acc[3] + 128) >> 8) << 24);
-    } else {
-        for (int i = 0; i < 4; i++) {
-            const int px = px0 + i;
-            if (px < -kPad || px >= D.w + kPad) continue;             // row margin: value unused
-            o |= pyr_px(src, S.pitch, r101(px, D.w), cy) << (8 * i);
+    }
+    const int cA = kXOff / 16;
+    int cB = a.aligned ? (w + kXOff - 16) / 16 : cA - 1;
+    if (cB < cA) cB = cA - 1;
+    const int ni = cB - cA + 1;
+    if (FRAME && ni > 0) {
+        const float rci = 1.f / (float)ni;
+        const int n1 = NR * ni;
+        for (int base = 0; base < n1; base += 256 * K) {
+            uint32_t v[K][VW];
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const int item = base + k * 256 + tid;
+                if (item < n1) {
+                    const int i = fdiv(item, ni, rci), c = cA + item - i * ni;
+                    const uint8_t* s = src + (long long)r101s(r0 - 2 + i, h) * a.stride + (16 * c - kXOff) * (COLOR ? 3 : 1);
+                    const u4a4k* q = reinterpret_cast<const u4a4k*>(s);
+                    const u4a4k t0 = q[0];
+                    v[k][0] = t0.x; v[k][1] = t0.y; v[k][2] = t0.z; v[k][3] = t0.w;
+                    if constexpr (COLOR) {
+                        const u4a4k t1 = q[1], t2 = q[2];
+                        v[k][4] = t1.x; v[k][5] = t1.y; v[k][6] = t1.z; v[k][7] = t1.w;
+                        v[k][8] = t2.x; v[k][9] = t2.y; v[k][10] = t2.z; v[k][11] = t2.w;
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const int item = base + k * 256 + tid;
+                if (item >= n1) continue;
+                const int i = fdiv(item, ni, rci), c = cA + item - i * ni;
+                uint32_t o[4] = {v[k][0], v[k][1], v[k][2], v[k][3]};
+                if constexpr (COLOR) {
+                    const uint8_t* bb = reinterpret_cast<const uint8_t*>(v[k]);
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        uint32_t d = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) d |= (uint32_t)gray_of(bb + 3 * (4 * t + j), fmt) << (8 * j);
+                        o[t] = d;
+                    }
+                }
+                *reinterpret_cast<uint4*>(lds + i * a.lp + 16 * c) = make_uint4(o[0], o[1], o[2], o[3]);
+            }
         }
     }
-    uint8_t* row = slab + D.img_off + (long long)(py + kPad) * D.pitch;
-    *reinterpret_cast<uint32_t*>(row + 4 * c) = o;
+    if constexpr (FRAME) {
+        // border bytes one per lane: columns -48 .. 16 cA - 65 and 16 (cB + 1) - 64 .. 16 nc0 - 49
+        const int nl = 16 * (cA - 1), nb = nl + 16 * (nc0 - cB);
+        const float rcb = 1.f / (float)nb;
+#pragma unroll 4
+        for (int item = tid; item < NR * nb; item += 256) {
+            const int i = fdiv(item, nb, rcb), e = item - i * nb;
+            const int x = e < nl ? e - 48 : 16 * (cB + 1) - kXOff + (e - nl);
+            const bool in = x >= -kPad && x < w + kPad;                     // row margin: left 0
+            const uint8_t* sp = src + (long long)r101s(r0 - 2 + i, h) * a.stride;
+            const int sx = in ? r101s(x, w) : 0;
+            uint32_t v;
+            if constexpr (COLOR) v = (uint32_t)gray_of(sp + 3 * sx, fmt);
+            else v = sp[sx];
+            lds[i * a.lp + kXOff + x] = (uint8_t)(in ? v : 0u);
+        }
+    }
+    __syncthreads();
+
+    // phase 2: level-0 rows out of LDS (core row r sits at LDS row r - r0 + 2)
+    if constexpr (FRAME) {
+        const int n0 = nb0 + (e0 - r0), n2 = n0 * nc0;
+        const float rc0 = 1.f / (float)nc0;
+        uint8_t* base0 = slab + a.L0.img_off;
+        for (int item = tid; item < n2; item += 256) {
+            const int j = fdiv(item, nc0, rc0), c = 1 + item - j * nc0;
+            const int py = out0[j];
+            const int i = r101s(py, h) - r0 + 2;
+            *reinterpret_cast<uint4*>(base0 + (long long)(py + kPad) * a.L0.pitch + 16 * c) =
+                *reinterpret_cast<const uint4*>(lds + i * a.lp + 16 * c);
+        }
+    }
+
+    // phase 3a: the band's level-1 core rows into an LDS row buffer.  A thread owns one dword
+    // chunk (4 level-1 pixels) of every row and walks down the band: each staged level-0 row's
+    // horizontal 5-tap sums (two chained v_dot4_u32_u8 per pixel) are computed once and kept in
+    // registers for the up to three level-1 rows whose vertical window covers it.
+    uint8_t* l1buf = lds + NR * a.lp;
+    {
+        const int nq = (w1 + 3) >> 2;
+        for (int q = tid; q < nq; q += 256) {
+            const int px0 = 4 * q;
+            const uint8_t* col = lds + kXOff + 2 * px0 - 4;      // level-0 columns 2 px0 - 4 .. 2 px0 + 11
+            uint32_t hr[5][4];
+            auto hsum = [&](int r, uint32_t (&o)[4]) {
+                const uint32_t* p = reinterpret_cast<const uint32_t*>(col + r * a.lp);
+                const uint32_t wd[4] = {p[0], p[1], p[2], p[3]};
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) {
+                    const int b0 = 2 * jj + 2, qq = b0 >> 2;
+                    const uint32_t lo = (b0 & 3) ? __builtin_amdgcn_alignbit(wd[qq + 1], wd[qq], 16) : wd[qq];
+                    const uint32_t hi = (b0 & 3) ? (wd[qq + 1] >> 16) : wd[qq + 1];
+                    o[jj] = __builtin_amdgcn_udot4(hi, 1u, __builtin_amdgcn_udot4(lo, 0x04060401u, 0u, false), false);
+                }
+            };
+            hsum(0, hr[0]);
+            hsum(1, hr[1]);
+            hsum(2, hr[2]);
+#pragma unroll
+            for (int yy = 0; yy < RB; yy++) {
+                if (Y0 + yy >= e1) break;
+                hsum(2 * yy + 3, hr[3]);
+                hsum(2 * yy + 4, hr[4]);
+                uint32_t o = 0;
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) {
+                    const uint32_t acc = hr[0][jj] + hr[1][jj] * 4u + hr[2][jj] * 6u + hr[3][jj] * 4u + hr[4][jj];
+                    o |= ((acc + 128) >> 8) << (8 * jj);
+                }
+                *reinterpret_cast<uint32_t*>(l1buf + yy * a.lp1 + kXOff + px0) = o;
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) {
+                    hr[0][jj] = hr[2][jj];
+                    hr[1][jj] = hr[3][jj];
+                    hr[2][jj] = hr[4][jj];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // phase 3a': the row buffer's reflect-101 borders (and zeroed margins), one byte per lane
+    {
+        const int nl = 48, nb = nl + 16 * (a.nchunk1_16 + 1) - kXOff - w1;   // columns -48..-1, w1..
+        const float rcb = 1.f / (float)nb;
+        const int nrow = e1 - Y0;
+        for (int item = tid; item < nrow * nb; item += 256) {
+            const int i = fdiv(item, nb, rcb), e = item - i * nb;
+            const int x = e < nl ? e - 48 : w1 + (e - nl);
+            const bool in = x >= -kPad && x < w1 + kPad;
+            uint8_t* row = l1buf + i * a.lp1 + kXOff;
+            const uint8_t v = row[in ? r101s(x, w1) : 0];
+            row[x] = in ? v : (uint8_t)0;
+        }
+    }
+    __syncthreads();
+
+    // phase 3b: level-1 padded rows out of the row buffer, 16 B per lane (borders by reflect-101
+    // in LDS; bytes 16..23 of a row are margin, written with zeros)
+    {
+        const int nc16 = a.nchunk1_16;                                // 16-B chunks 1 .. nc16
+        const float rc16 = 1.f / (float)nc16;
+        const int n3 = (nb1 + (e1 - Y0)) * nc16;
+        uint8_t* base1 = slab + a.L1.img_off;
+        for (int item = tid; item < n3; item += 256) {
+            const int j = fdiv(item, nc16, rc16), c = 1 + item - j * nc16;
+            const int py = out1[j];
+            const uint8_t* row = l1buf + (r101s(py, h1) - Y0) * a.lp1 + kXOff;
+            const int px0 = 16 * c - kXOff;
+            const uint4 o = *reinterpret_cast<const uint4*>(row + px0);
+            *reinterpret_cast<uint4*>(base1 + (long long)(py + kPad) * a.L1.pitch + 16 * c) = o;
+        }
+    }
 }
 
 // ------------------------------------------------------------------ A3: Scharr derivs
@@ -897,13 +1122,66 @@ hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const u
     return hipGetLastError();
 }
 
-hipError_t launch_pyrdown(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int level, int fsel)
+// k_front's band height: 4 destination rows while a band's LDS fits 32 KB (5-6 bands per CU),
+// else 2.  At 1080p x 32 one frame side of gray + pad + level 1 takes 44 us against 56 with 8 rows
+// and 107 for k_gray_pad + k_pyrdown (scripts/micro/front_bench.hip).
+static hipError_t launch_front_bands(hipStream_t s, FrontArgs& a, int mode)
 {
-    const Level& D = g.lv[level];
-    const int nchunk = (kXOff + D.w + kPad - 1) / 4;                 // last dword chunk
-    const dim3 grid((nchunk - 6 + 1 + 63) / 64, D.h + 2 * kPad, fsel ? batch : 2 * batch);
-    hipLaunchKernelGGL(k_pyrdown, grid, dim3(64), 0, s, pyr1, pyr2, g.img_bytes, g.lv[level - 1], D, nchunk, fsel);
+    const bool wide = (2 * 4 + 3) * a.lp + 4 * a.lp1 > 32 * 1024;
+    const int rb = wide ? 2 : 4;
+    a.nbands = (a.L1.h + rb - 1) / rb;
+    const dim3 grid((unsigned)(a.nbands * a.nz));
+    const size_t lds = (size_t)(2 * rb + 3) * a.lp + (size_t)rb * a.lp1;
+#define MDX_FRONT_CASE(M)                                                              \
+    if (mode == M) {                                                                   \
+        if (wide) hipLaunchKernelGGL((k_front<2, M>), grid, dim3(256), lds, s, a);     \
+        else hipLaunchKernelGGL((k_front<4, M>), grid, dim3(256), lds, s, a);          \
+    }
+    MDX_FRONT_CASE(0) MDX_FRONT_CASE(1) MDX_FRONT_CASE(2)
+#undef MDX_FRONT_CASE
     return hipGetLastError();
+}
+
+static FrontArgs front_args(int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int src_level, int fsel)
+{
+    FrontArgs a{};
+    a.fsel = fsel;
+    a.img_bytes = g.img_bytes;
+    a.pyr1 = pyr1;
+    a.pyr2 = pyr2;
+    a.L0 = g.lv[src_level];
+    a.L1 = g.lv[src_level + 1];
+    a.w = a.L0.w;
+    a.h = a.L0.h;
+    a.nchunk0 = last_chunk16(a.L0.w);
+    a.nchunk1_16 = last_chunk16(a.L1.w);
+    a.lp = 16 * (a.nchunk0 + 1);
+    a.lp1 = 16 * (a.nchunk1_16 + 1);
+    a.nz = fsel ? batch : 2 * batch;
+    return a;
+}
+
+hipError_t launch_front(hipStream_t s, int batch, const uint8_t* in1, const uint8_t* in2, int w, int h, int stride,
+                        long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int fsel)
+{
+    if (g.nlev < 2) return launch_gray_pad(s, batch, in1, in2, w, h, stride, frame_stride, fmt, pyr1, pyr2, g, fsel);
+    FrontArgs a = front_args(batch, pyr1, pyr2, g, 0, fsel);
+    a.in1 = in1;
+    a.in2 = in2;
+    a.stride = stride;
+    a.fmt = fmt;
+    a.frame_stride = frame_stride;
+    a.aligned = ((((uintptr_t)in1 | (uintptr_t)in2) & 3) == 0 && (stride & 3) == 0 && (frame_stride & 3) == 0) ? 1 : 0;
+    return launch_front_bands(s, a, fmt == MDX_FMT_GRAY8 ? 0 : 1);
+}
+
+hipError_t launch_pyr_levels(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int fsel)
+{
+    for (int l = 2; l < g.nlev; l++) {
+        FrontArgs a = front_args(batch, pyr1, pyr2, g, l - 1, fsel);
+        if (hipError_t e = launch_front_bands(s, a, 2)) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level)
