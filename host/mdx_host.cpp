@@ -48,6 +48,7 @@ MotionDetectionNode::MotionDetectionNode(const Params& p, int device, int max_w,
     mdx_default_params(&mp);
     mp.pixel_step = p_.pixel_step;
     mp.min_vector_size = p_.min_vector_size;
+    mp.subspace_precision = p_.subspace_precision;
     ctx_ = mdx_create(device, max_w, max_h, 1, &mp);
     if (!ctx_) throw std::runtime_error(std::string("mdx_create: ") + mdx_create_error());
     mdx_srand(&rng_, p_.seed);

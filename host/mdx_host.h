@@ -52,6 +52,7 @@ struct Params {
     // caller that produces the motion mask
     bool live_path = true;
     uint32_t seed = 1;             // the reference seeds rand() with time(NULL) (outlier_detector.cpp:17)
+    int subspace_precision = MDX_SUBSPACE_F64;   // or MDX_SUBSPACE_F32 (the reference's float shape)
 };
 
 // One processed frame's outputs (what the node hands to its publishers / logs).

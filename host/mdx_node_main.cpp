@@ -3,6 +3,7 @@
 //
 //   mdx_node <frames.bin> <outdir> [pixel_step=10] [min_vector_size=1.0] [skip_frames=1]
 //            [num_motions=2] [egomotion=1] [live_path=1] [sigma=0.5] [seed=1] [device=0]
+//            [subspace_precision=0]   (0 double, 1 the reference's float arithmetic shape)
 //
 // frames.bin: "MDXF", u32 count, then per frame u32 height, u32 width, u32 step, u32 len, the
 // encoding (len bytes) and step * height data bytes (a sensor_msgs/Image each).
@@ -86,6 +87,7 @@ int main(int argc, char** argv)
         p.live_path = std::atoi(get("live_path", "1").c_str()) != 0;
         p.sigma = std::atof(get("sigma", "0.5").c_str());
         p.seed = (uint32_t)std::strtoul(get("seed", "1").c_str(), nullptr, 10);
+        p.subspace_precision = std::atoi(get("subspace_precision", "0").c_str());
         const int device = std::atoi(get("device", "0").c_str());
         const std::string out = argv[2];
         const std::vector<Image> frames = read_frames(argv[1]);

@@ -46,6 +46,11 @@ extern "C" {
                                 vectors in x-major grid order (:120) */
 #define MDX_FIT_EXTERNAL 1   /* caller supplies H (forward, frame1 -> frame2) per pair */
 
+/* mdx_fit_subspace arithmetic (see its comment below). */
+#define MDX_SUBSPACE_F64 0   /* double Householder basis and residuals (stable; the default) */
+#define MDX_SUBSPACE_F32 1   /* the reference's float arithmetic shape: Eigen::MatrixXf
+                                (outlier_detector.cpp:243-290), Pnd formed explicitly in float */
+
 typedef struct {
     int    win;              /* LK window side; reference hard-codes 40 (:41). Only 40 is supported. */
     int    max_level;        /* reference MAX_LEVEL = 5 (:40) */
@@ -56,6 +61,7 @@ typedef struct {
     int    pixel_step;       /* ROS param pixel_step (node.cpp:29; 10 in bag.launch:27) */
     double min_vector_size;  /* ROS param min_vector_size, default 1.0 (node.cpp:44) */
     int    fit_mode;         /* MDX_FIT_FIRST4 (default) or MDX_FIT_EXTERNAL */
+    int    subspace_precision; /* mdx_fit_subspace arithmetic: MDX_SUBSPACE_F64 (default) or _F32 */
 } mdx_params;
 
 typedef struct mdx_ctx mdx_ctx;
@@ -210,8 +216,11 @@ int mdx_flow_trajectory(mdx_ctx* ctx, const uint8_t* const* imgs, int nimg, int 
  *   is_outlier  [ntraj] 1 where the winner's residual exceeds sigma^2 * chi2_99[n-d]
  *   residuals   [ntraj] double, the winner's residuals
  *   outlier_points [n_outliers][2] float: each outlier's second-to-last point (:322), in order
- * Arithmetic: the reference's float meanSubtract; double Householder QR of each sample and
- * double residuals (the reference: Eigen float JacobiSVD; see DESIGN.md §7c for parity).
+ * Arithmetic: the reference's float meanSubtract, then by mdx_params.subspace_precision:
+ * MDX_SUBSPACE_F64 -- double Householder QR of each sample and double residuals; MDX_SUBSPACE_F32
+ * -- the reference's float shape (float basis, explicit float Pnd = I - sum u u', float x'(Pnd x)).
+ * The reference itself runs Eigen's float JacobiSVD, which neither mode restates rotation for
+ * rotation.
  */
 typedef struct mdx_rand_state { uint32_t x[34]; int32_t pos; } mdx_rand_state;
 void mdx_srand(mdx_rand_state* st, uint32_t seed);

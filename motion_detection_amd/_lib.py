@@ -25,6 +25,7 @@ MDX_EDEGENERATE = 1
 
 FMT_GRAY8, FMT_RGB8, FMT_BGR8 = 0, 1, 2
 FIT_FIRST4, FIT_EXTERNAL = 0, 1
+SUBSPACE_F64, SUBSPACE_F32 = 0, 1
 
 # every symbol include/mdx.h declares (checked by tests/test_abi.py)
 EXPORTED = [
@@ -60,7 +61,7 @@ assert C.sizeof(MdxBandCand) == BAND_CAND_BYTES
 class MdxParams(C.Structure):
     _fields_ = [("win", C.c_int), ("max_level", C.c_int), ("max_iters", C.c_int), ("eps", C.c_double),
                 ("min_eig", C.c_float), ("thresh", C.c_int), ("pixel_step", C.c_int),
-                ("min_vector_size", C.c_double), ("fit_mode", C.c_int)]
+                ("min_vector_size", C.c_double), ("fit_mode", C.c_int), ("subspace_precision", C.c_int)]
 
 
 class MdxError(RuntimeError):

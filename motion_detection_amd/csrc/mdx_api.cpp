@@ -84,6 +84,7 @@ extern "C" void mdx_default_params(mdx_params* p)
     p->pixel_step = 10;
     p->min_vector_size = 1.0;
     p->fit_mode = MDX_FIT_FIRST4;
+    p->subspace_precision = MDX_SUBSPACE_F64;
 }
 
 extern "C" int mdx_grid_count(int w, int h, int ps)
@@ -98,6 +99,10 @@ static int check_params(const mdx_params* p, std::string* why)
     if (p->max_level < 0 || p->max_level >= kMaxLevels) { *why = "max_level out of range [0, 7]"; return 0; }
     if (p->pixel_step <= 0) { *why = "pixel_step must be > 0 (reference leaves it unset: UB)"; return 0; }
     if (p->fit_mode != MDX_FIT_FIRST4 && p->fit_mode != MDX_FIT_EXTERNAL) { *why = "bad fit_mode"; return 0; }
+    if (p->subspace_precision != MDX_SUBSPACE_F64 && p->subspace_precision != MDX_SUBSPACE_F32) {
+        *why = "bad subspace_precision";
+        return 0;
+    }
     return 1;
 }
 
@@ -788,7 +793,8 @@ extern "C" int mdx_fit_subspace(mdx_ctx* c, const float* traj, int ntraj, int tr
     int rc;
     if ((rc = ensure(c, c->straj, N * n * 4)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->sdata, N * n * 4)) != MDX_OK) return rc;
-    if ((rc = ensure(c, c->sq, (size_t)kHyp * n * std::max(n - d, 1) * 8)) != MDX_OK) return rc;
+    const size_t qb = std::max((size_t)n * std::max(n - d, 1) * 8, (size_t)n * n * 4);   // F64 basis / F32 Pnd
+    if ((rc = ensure(c, c->sq, (size_t)kHyp * qb)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->scnt, kHyp * 4)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->scols, cols.size() * 4)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->sres, N * 8)) != MDX_OK) return rc;
@@ -799,7 +805,7 @@ extern "C" int mdx_fit_subspace(mdx_ctx* c, const float* traj, int ntraj, int tr
     HIP_OR_RETURN(c, hipMemcpyAsync(c->scols.p, cols.data(), cols.size() * 4, hipMemcpyHostToDevice, s));
     HIP_OR_RETURN(c, launch_subspace(s, c->straj.as<float>(), ntraj, traj_len, d, c->scols.as<int>(), kHyp, sigma,
                                      c->sdata.as<float>(), c->sq.as<double>(), c->scnt.as<int>(), c->sres.as<double>(),
-                                     c->sout.as<uint8_t>(), c->sbest.as<int>()));
+                                     c->sout.as<uint8_t>(), c->sbest.as<int>(), c->prm.subspace_precision));
     std::vector<uint8_t> out(N);
     int best = -1;
     HIP_OR_RETURN(c, hipMemcpyAsync(out.data(), c->sout.p, N, hipMemcpyDeviceToHost, s));

@@ -121,10 +121,10 @@ hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
 // Trajectory subspace RANSAC (fitSubspace): mean-subtracted data, nhyp hypotheses of d columns
 // (cols: [nhyp][d]), winner's residuals / outlier flags; best[0] = winner or -1.  Scratch: data
-// [N][2T] floats, qbuf [nhyp][2T][2T-d] doubles, counts [nhyp].
+// [N][2T] floats, qbuf [nhyp][2T][2T-d] doubles (MDX_SUBSPACE_F32: [nhyp][2T][2T] floats), counts [nhyp].
 hipError_t launch_subspace(hipStream_t s, const float* traj, int N, int T, int d, const int* cols, int nhyp,
                            double sigma, float* data, double* qbuf, int* counts, double* residuals,
-                           uint8_t* is_outlier, int* best);
+                           uint8_t* is_outlier, int* best, int precision);
 // Trajectory tracking (calculateOpticalFlowTrajectory): grid init and the per-pass point update.
 hipError_t launch_traj_init(hipStream_t s, int npts, int ny, int pixel_step, int nimg, float* cur, float* traj,
                             int* tlen, int* num);

@@ -101,26 +101,13 @@ __device__ __forceinline__ uint32_t quad_bcast_u(uint32_t v)
 // must be kept from moving LDS accesses across it (no s_barrier, no forced vmcnt(0)).
 __device__ __forceinline__ void wave_lds_fence()
 {
-#ifdef LKX_SYNC
-    __syncthreads();
-#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
 }
 
-// timing-only builds (scripts/lk_variants.sh): LKX_MEMFREE re-reads one row (cache-resident) in
-// the iteration kernel, which bounds what hiding the load latency could gain
-#ifdef LKX_MEMFREE
-#define LKX_ROWSTEP(x) 0u
-#else
-#define LKX_ROWSTEP(x) (x)
-#endif
-
-#ifndef LKX_WPE_ITER
-#define LKX_WPE_ITER 5   // k_lk_iter: 5 waves/SIMD (<= 102 VGPRs; measured 3% faster than 6 at <= 80)
-#endif
+// k_lk_iter: 5 waves/SIMD (<= 102 VGPRs; measured 3% faster than 6 at <= 80)
+constexpr int kLkIterWavesPerEU = 5;
 typedef __attribute__((address_space(3))) void* lds_ptr;
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 // volatile LDS views: each access stays one ds_read_b64 / ds_read_b128 (never merged into a
@@ -131,9 +118,7 @@ typedef __attribute__((address_space(3))) volatile const v4u lds_u4v;
 __device__ __forceinline__ void lk_vmcnt0()
 {
     __builtin_amdgcn_sched_barrier(0);
-#ifndef LKX_NOWAIT   // timing-only builds: measure what the row waits cost (results invalid)
     __builtin_amdgcn_s_waitcnt(0x0F70);
-#endif
     __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -395,7 +380,7 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
 // would halve the LDS rate) and the quad's J dwords with three ds_read_b128.  D and C travel as
 // one pair, so a chain element is one 2-cycle LDS access (it was two read2_b32 halves).
 template <int G, int UW>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER, 8))) void k_lk_iter(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWavesPerEU, 8))) void k_lk_iter(
     LkArgs a, const uint8_t* __restrict__ cls, const float4* __restrict__ Ab, int* __restrict__ qctr, int level,
     int ngroups, int batch)
 {
@@ -509,16 +494,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER
         f2 acc = {0.f, 0.f};
         if (act) iters++;
         int inx = (int)floorf(nx), iny = (int)floorf(ny);
-#ifdef LKX_FIXED   // timing-only: data-independent work (points never leave early, addresses clamped)
-        inx = min(max(inx, -kWin), L.w - 1);
-        iny = min(max(iny, -kWin), L.h - 1);
-        if (!(nx == nx)) { inx = 0; iny = 0; }
-#else
         if (act && (inx < -kWin || inx >= L.w || iny < -kWin || iny >= L.h)) {
             act = false;
             if (level == 0) status = 0;
         }
-#endif
         if (!act) { inx = 0; iny = 0; }
         const float fa = nx - (float)inx, fb = ny - (float)iny;
         int v00, v01, v10, v11;
@@ -542,23 +521,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER
             }
         }
         auto dma_union = [&](int b) {
-#if defined(LKX_NODMA) || defined(LKX_NODMA_U)   // timing-only builds: no row staging (results invalid)
-            if (uoff[0] != 0x7fffffffu) return;
-#endif
 #pragma unroll
             for (int c = 0; c < ND; c++) {
                 if (c < ND - 1 || 1024 * c + 16 * lane < Sh::BYTES)
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)&dU[b][256 * c], 16, (int)uoff[c], 0, 0, 0);
-                uoff[c] += LKX_ROWSTEP(rowb);
+                uoff[c] += rowb;
             }
         };
         auto dma_j = [&](int b) {
-#if defined(LKX_NODMA) || defined(LKX_NODMA_J)
-            if (joff != 0x7fffffffu) return;
-#endif
             // the quad's taps span 44 bytes: lanes 0-2 carry them, lane 3 stays idle
             if (k < 3) __builtin_amdgcn_raw_ptr_buffer_load_lds(jrs, (lds_ptr)&dJ[b][0], 16, (int)joff, 0, 0, 0);
-            joff += LKX_ROWSTEP((uint32_t)pitch);
+            joff += (uint32_t)pitch;
         };
         lds_u4v* lJ = (lds_u4v*)&dJ[0][(lane >> 2) * 16];
         auto read_j = [&](int b, uint32_t (&rj)[11]) {
@@ -627,9 +600,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER
             ny = ny + dy;
             npx = nx + HALFW;
             npy = ny + HALFW;
-#ifdef LKX_FIXED   // timing-only builds: every trackable point iterates exactly LKX_FIXED times
-            if (j + 1 >= LKX_FIXED) act = false;
-#else
             if ((double)dx * dx + (double)dy * dy <= a.eps2) {
                 act = false;
             } else if (j > 0 && fabs((double)fabsf(dx + pdx)) < 0.01 && fabs((double)fabsf(dy + pdy)) < 0.01) {
@@ -637,7 +607,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LKX_WPE_ITER
                 npy = npy - dy * 0.5f;
                 act = false;
             }
-#endif
             pdx = dx;
             pdy = dy;
         }

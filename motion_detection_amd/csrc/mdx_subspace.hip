@@ -11,6 +11,8 @@
 //   winner    the first hypothesis with the most inliers (strict >, :300); outliers: its residual
 //             > sigma^2 chi2_99[n - d] (:312-323)                            -> k_subspace_final
 //
+// Precision MDX_SUBSPACE_F64 (default) as above; MDX_SUBSPACE_F32 follows the reference's float
+// arithmetic shape instead (explicit float Pnd, see k_subspace_hyp_f32).
 // One workgroup per hypothesis: lane 0 factors the tiny n x d sample (n <= 32) in double, the
 // workgroup then streams all N columns (2n MACs each) and reduces its inlier count.  The double
 // arithmetic follows the oracle's restatement (oracle/mdx_oracle.c subspace_basis /
@@ -134,6 +136,103 @@ __device__ __forceinline__ double subspace_residual(const double* q2, int n, int
     return res;
 }
 
+// Float mode (MDX_SUBSPACE_F32): the reference's float arithmetic shape -- the sample's Householder
+// basis in float, Pnd = I - sum_idx u u' formed explicitly (outlier_detector.cpp:272-282) and the
+// residual |x' (Pnd x)| as the two float products of :286.  Statement for statement the oracle's
+// subspace_pnd_f32 / subspace_residual_f32 (oracle/mdx_oracle.c), un-fused.  P: n x n row-major.
+__device__ void subspace_pnd_f32(float* A, int n, int d, float* V, float* beta, float* q, float* P)
+{
+    for (int k = 0; k < d; k++) {
+        float nrm2 = 0.0f;
+        for (int r = k; r < n; r++) nrm2 = nrm2 + A[k * n + r] * A[k * n + r];
+        const float nrm = __builtin_sqrtf(nrm2);
+        const float x0 = A[k * n + k];
+        const float alpha = x0 >= 0.0f ? -nrm : nrm;
+        for (int r = k; r < n; r++) V[k * n + r] = A[k * n + r];
+        V[k * n + k] = x0 - alpha;
+        float b = 0.0f;
+        for (int r = k; r < n; r++) b = b + V[k * n + r] * V[k * n + r];
+        beta[k] = b;
+        if (b == 0.0f) continue;
+        for (int c = k; c < d; c++) {
+            float dot = 0.0f;
+            for (int r = k; r < n; r++) dot = dot + V[k * n + r] * A[c * n + r];
+            const float f = 2.0f * dot / b;
+            for (int r = k; r < n; r++) A[c * n + r] = A[c * n + r] - f * V[k * n + r];
+        }
+    }
+    for (int e = 0; e < n * n; e++) P[e] = 0.0f;
+    for (int j = 0; j < d; j++) {
+        for (int r = 0; r < n; r++) q[r] = r == j ? 1.0f : 0.0f;
+        for (int k = d - 1; k >= 0; k--) {
+            if (beta[k] == 0.0f) continue;
+            float dot = 0.0f;
+            for (int r = k; r < n; r++) dot = dot + V[k * n + r] * q[r];
+            const float f = 2.0f * dot / beta[k];
+            for (int r = k; r < n; r++) q[r] = q[r] - f * V[k * n + r];
+        }
+        for (int a = 0; a < n; a++)
+            for (int b = 0; b < n; b++) P[a * n + b] = P[a * n + b] + q[a] * q[b];
+    }
+    for (int a = 0; a < n; a++)
+        for (int b = 0; b < n; b++) P[a * n + b] = (a == b ? 1.0f : 0.0f) - P[a * n + b];
+}
+
+__device__ __forceinline__ float subspace_residual_f32(const float* P, int n, const float* x)
+{
+    float res = 0.0f;
+    for (int a = 0; a < n; a++) {
+        float y = 0.0f;
+        for (int b = 0; b < n; b++) y = y + P[a * n + b] * x[b];
+        res = res + x[a] * y;
+    }
+    return __builtin_fabsf(res);
+}
+
+// float mode of k_subspace_hyp: pbuf [nhyp][n][n] floats (each hypothesis' Pnd)
+__global__ __launch_bounds__(256) void k_subspace_hyp_f32(const float* __restrict__ data, int N, int n, int d,
+                                                           const int* __restrict__ cols, double inlier_thr,
+                                                           float* __restrict__ pbuf, int* __restrict__ counts)
+{
+    __shared__ float sA[kMaxSub * kMaxSub], sV[kMaxSub * kMaxSub], sbeta[kMaxSub], sq[kMaxSub];
+    __shared__ float sP[kMaxSub * kMaxSub];
+    __shared__ int s_cnt[4];
+    const int h = blockIdx.x, tid = threadIdx.x;
+    for (int e = tid; e < n * d; e += 256) {
+        const int k = e / n, r = e - k * n;
+        sA[e] = data[(long long)cols[h * d + k] * n + r];
+    }
+    __syncthreads();
+    if (tid == 0) subspace_pnd_f32(sA, n, d, sV, sbeta, sq, sP);
+    __syncthreads();
+    for (int e = tid; e < n * n; e += 256) pbuf[(long long)h * n * n + e] = sP[e];
+    int cnt = 0;
+    for (int i = tid; i < N; i += 256)
+        if ((double)subspace_residual_f32(sP, n, data + (long long)i * n) < inlier_thr) cnt++;
+    for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if ((tid & 63) == 0) s_cnt[tid >> 6] = cnt;
+    __syncthreads();
+    if (tid == 0) counts[h] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+}
+
+__global__ __launch_bounds__(256) void k_subspace_final_f32(const float* __restrict__ data, int N, int n, int nhyp,
+                                                             const int* __restrict__ counts,
+                                                             const float* __restrict__ pbuf, double out_thr,
+                                                             double* __restrict__ residuals,
+                                                             uint8_t* __restrict__ is_outlier, int* __restrict__ best)
+{
+    int bh = -1, bc = 0;
+    for (int h = 0; h < nhyp; h++)
+        if (counts[h] > bc) { bc = counts[h]; bh = h; }
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) best[0] = bh;
+    if (i >= N) return;
+    double r = 0.0;
+    if (bh >= 0) r = (double)subspace_residual_f32(pbuf + (long long)bh * n * n, n, data + (long long)i * n);
+    if (residuals) residuals[i] = r;
+    is_outlier[i] = (uint8_t)(bh >= 0 && r > out_thr);
+}
+
 // grid: one workgroup per hypothesis.  cols: [nhyp][d] sample indices; qbuf: [nhyp][n][n-d];
 // counts: [nhyp] inliers.
 __global__ __launch_bounds__(256) void k_subspace_hyp(const float* __restrict__ data, int N, int n, int d,
@@ -184,7 +283,7 @@ __global__ __launch_bounds__(256) void k_subspace_final(const float* __restrict_
 
 hipError_t launch_subspace(hipStream_t s, const float* traj, int N, int T, int d, const int* cols, int nhyp,
                            double sigma, float* data, double* qbuf, int* counts, double* residuals,
-                           uint8_t* is_outlier, int* best)
+                           uint8_t* is_outlier, int* best, int precision)
 {
     const int n = 2 * T;
     // n - d == 10: the reference's chi_square_table.at(0).at(10) throws (outlier_detector.cpp:315)
@@ -194,6 +293,14 @@ hipError_t launch_subspace(hipStream_t s, const float* traj, int N, int T, int d
     static const double p99[10] = {0.0, 0.020, 0.115, 0.297, 0.554, 0.872, 1.239, 1.646, 2.088, 2.558};
     const double out_thr = (n - d > 0 && n - d < 10) ? sigma * sigma * p99[n - d] : 0.2;
     hipLaunchKernelGGL(k_subspace_prep, dim3(1), dim3(256), 0, s, traj, N, T, data);
+    if (precision == MDX_SUBSPACE_F32) {
+        float* pbuf = reinterpret_cast<float*>(qbuf);
+        hipLaunchKernelGGL(k_subspace_hyp_f32, dim3(nhyp), dim3(256), 0, s, data, N, n, d, cols, inlier_thr, pbuf,
+                           counts);
+        hipLaunchKernelGGL(k_subspace_final_f32, dim3((N + 255) / 256), dim3(256), 0, s, data, N, n, nhyp, counts,
+                           pbuf, out_thr, residuals, is_outlier, best);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_subspace_hyp, dim3(nhyp), dim3(256), 0, s, data, N, n, d, cols, inlier_thr, qbuf, counts);
     hipLaunchKernelGGL(k_subspace_final, dim3((N + 255) / 256), dim3(256), 0, s, data, N, n, d, nhyp, counts, qbuf,
                        out_thr, residuals, is_outlier, best);

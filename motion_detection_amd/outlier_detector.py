@@ -28,7 +28,10 @@ from .context import Context, SubspaceResult
 
 
 class OutlierDetector:
-    def __init__(self, seed: int | None = None, device: int = 0):
+    def __init__(self, seed: int | None = None, device: int = 0, precision: int = _lib.SUBSPACE_F64):
+        """precision: SUBSPACE_F64 (default, stable) or SUBSPACE_F32 (the reference's float
+        arithmetic shape; see include/mdx.h mdx_fit_subspace)."""
+        self.precision = int(precision)
         self.rng = _lib.MdxRandState()
         self.seed = int(time.time()) & 0xFFFFFFFF if seed is None else int(seed) & 0xFFFFFFFF
         _lib.lib().mdx_srand(C.byref(self.rng), self.seed)
@@ -39,7 +42,7 @@ class OutlierDetector:
     def fitSubspace(self, trajectories, outlier_points: list, num_motions: int, sigma: float) -> list:
         traj = np.ascontiguousarray(np.asarray(trajectories, dtype=np.float32))
         if self._ctx is None:
-            self._ctx = Context(self._device, 64, 64, 1)
+            self._ctx = Context(self._device, 64, 64, 1, subspace_precision=self.precision)
         res = self._ctx.fit_subspace(traj, num_motions, sigma, self.rng)
         self.last = res
         outlier_points.extend(tuple(p) for p in res.outlier_points)

@@ -1016,6 +1016,64 @@ static double subspace_residual(const double* q2, int n, int m, const float* x)
     return res;
 }
 
+/* Float mode (ORA_SUBSPACE_F32): the reference's float arithmetic shape (outlier_detector.cpp:
+ * 243-290, every Eigen::MatrixXf/VectorXf quantity a float): the sample's basis from the same
+ * Householder statement in float; Pnd formed explicitly as I - sum_idx u u' with the sum taken
+ * idx by idx (:272-282: Pnd = Pnd + M, then Identity - Pnd); residual = |x' (Pnd x)| as the two
+ * products of :286 (y = Pnd x with sequential b, then x'y with sequential a), float throughout.
+ * Eigen's own JacobiSVD rotations and its vectorised GEMM order are not restated (Eigen is not in
+ * the reference tree to pin against): this mode reproduces the precision, not Eigen's exact
+ * bits, and the GPU kernel follows it operation for operation.  P: n x n row-major. */
+static void subspace_pnd_f32(float* A, int n, int d, float* P)
+{
+    float V[ORA_MAX_SUBSPACE * ORA_MAX_SUBSPACE], beta[ORA_MAX_SUBSPACE], q[ORA_MAX_SUBSPACE];
+    for (int k = 0; k < d; k++) {
+        float nrm2 = 0.0f;
+        for (int r = k; r < n; r++) nrm2 = nrm2 + A[k * n + r] * A[k * n + r];
+        const float nrm = sqrtf(nrm2);
+        const float x0 = A[k * n + k];
+        const float alpha = x0 >= 0.0f ? -nrm : nrm;
+        for (int r = k; r < n; r++) V[k * n + r] = A[k * n + r];
+        V[k * n + k] = x0 - alpha;
+        float b = 0.0f;
+        for (int r = k; r < n; r++) b = b + V[k * n + r] * V[k * n + r];
+        beta[k] = b;
+        if (b == 0.0f) continue;
+        for (int c = k; c < d; c++) {
+            float dot = 0.0f;
+            for (int r = k; r < n; r++) dot = dot + V[k * n + r] * A[c * n + r];
+            const float f = 2.0f * dot / b;
+            for (int r = k; r < n; r++) A[c * n + r] = A[c * n + r] - f * V[k * n + r];
+        }
+    }
+    for (int e = 0; e < n * n; e++) P[e] = 0.0f;
+    for (int j = 0; j < d; j++) {                  /* u_j = Q e_j, then Pnd = Pnd + u_j u_j' */
+        for (int r = 0; r < n; r++) q[r] = r == j ? 1.0f : 0.0f;
+        for (int k = d - 1; k >= 0; k--) {
+            if (beta[k] == 0.0f) continue;
+            float dot = 0.0f;
+            for (int r = k; r < n; r++) dot = dot + V[k * n + r] * q[r];
+            const float f = 2.0f * dot / beta[k];
+            for (int r = k; r < n; r++) q[r] = q[r] - f * V[k * n + r];
+        }
+        for (int a = 0; a < n; a++)
+            for (int b = 0; b < n; b++) P[a * n + b] = P[a * n + b] + q[a] * q[b];
+    }
+    for (int a = 0; a < n; a++)
+        for (int b = 0; b < n; b++) P[a * n + b] = (a == b ? 1.0f : 0.0f) - P[a * n + b];
+}
+
+static float subspace_residual_f32(const float* P, int n, const float* x)
+{
+    float res = 0.0f;
+    for (int a = 0; a < n; a++) {
+        float y = 0.0f;
+        for (int b = 0; b < n; b++) y = y + P[a * n + b] * x[b];
+        res = res + x[a] * y;
+    }
+    return fabsf(res);
+}
+
 /* meanSubtract (outlier_detector.cpp:200-221): float sums of row 0 / row 1 in column order,
  * double mean, float constants; even rows minus the x mean, odd rows = y mean minus the row (the
  * reference's y flip).  data: N columns of n floats (column i = trajectory i). */
@@ -1041,31 +1099,46 @@ void ora_subspace_data(const float* traj, int N, int T, float* data)
 int ora_fit_subspace(const float* traj, int N, int T, int num_motions, double sigma, ora_rand_state* rng,
                      int* columns, uint8_t* is_outlier, double* residuals)
 {
+    return ora_fit_subspace_ex(traj, N, T, num_motions, sigma, rng, columns, is_outlier, residuals, ORA_SUBSPACE_F64);
+}
+
+int ora_fit_subspace_ex(const float* traj, int N, int T, int num_motions, double sigma, ora_rand_state* rng,
+                        int* columns, uint8_t* is_outlier, double* residuals, int precision)
+{
     const int n = 2 * T, d = 4 * num_motions;
     if (N <= 0 || d <= 0 || d > n || n > ORA_MAX_SUBSPACE || n - d == 10) return -1;
     float* data = (float*)malloc(sizeof(float) * (size_t)N * n);
     double* best_res = (double*)malloc(sizeof(double) * (size_t)N);
     double* q2 = (double*)malloc(sizeof(double) * (size_t)n * (n - d > 0 ? n - d : 1));
     double A[ORA_MAX_SUBSPACE * ORA_MAX_SUBSPACE];
+    float Af[ORA_MAX_SUBSPACE * ORA_MAX_SUBSPACE], P[ORA_MAX_SUBSPACE * ORA_MAX_SUBSPACE];
     int cols[ORA_MAX_SUBSPACE];
+    const int f32 = precision == ORA_SUBSPACE_F32;
     ora_subspace_data(traj, N, T, data);
     const double inlier_thr = (double)(n - d) * sigma * sigma;
     int max_points = 0, have = 0;
     for (int it = 0; it < 50; it++) {
         for (int k = 0; k < d; k++) {
             cols[k] = ora_rand(rng) % N;
-            for (int r = 0; r < n; r++) A[k * n + r] = (double)data[(size_t)cols[k] * n + r];
+            for (int r = 0; r < n; r++) {
+                A[k * n + r] = (double)data[(size_t)cols[k] * n + r];
+                Af[k * n + r] = data[(size_t)cols[k] * n + r];
+            }
         }
-        subspace_basis(A, n, d, q2);
+        if (f32) subspace_pnd_f32(Af, n, d, P);
+        else subspace_basis(A, n, d, q2);
+#define ORA_RES(i) (f32 ? (double)subspace_residual_f32(P, n, data + (size_t)(i) * n) \
+                        : subspace_residual(q2, n, n - d, data + (size_t)(i) * n))
         int np = 0;
         for (int i = 0; i < N; i++)
-            if (subspace_residual(q2, n, n - d, data + (size_t)i * n) < inlier_thr) np++;
+            if (ORA_RES(i) < inlier_thr) np++;
         if (np > max_points) {
             max_points = np;
             have = 1;
             for (int k = 0; k < d; k++) columns[k] = cols[k];
-            for (int i = 0; i < N; i++) best_res[i] = subspace_residual(q2, n, n - d, data + (size_t)i * n);
+            for (int i = 0; i < N; i++) best_res[i] = ORA_RES(i);
         }
+#undef ORA_RES
     }
     /* chi-square 99% table (:19-30), indexed by n - d */
     static const double p99[10] = {0.0, 0.020, 0.115, 0.297, 0.554, 0.872, 1.239, 1.646, 2.088, 2.558};

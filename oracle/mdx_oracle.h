@@ -131,6 +131,12 @@ int  ora_rand(ora_rand_state* s);
 void ora_subspace_data(const float* traj, int N, int T, float* data);
 int  ora_fit_subspace(const float* traj, int N, int T, int num_motions, double sigma, ora_rand_state* rng,
                       int* columns, uint8_t* is_outlier, double* residuals);
+/* precision: ORA_SUBSPACE_F64 (the default above: double basis and residuals) or ORA_SUBSPACE_F32
+ * (the reference's float arithmetic shape, explicit Pnd; see subspace_pnd_f32) */
+#define ORA_SUBSPACE_F64 0
+#define ORA_SUBSPACE_F32 1
+int  ora_fit_subspace_ex(const float* traj, int N, int T, int num_motions, double sigma, ora_rand_state* rng,
+                         int* columns, uint8_t* is_outlier, double* residuals, int precision);
 
 /* Synthetic-frame generator spec is in the product (motion_detection_amd/csrc/synth.cpp);
  * the oracle does not need one. */

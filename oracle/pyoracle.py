@@ -83,6 +83,9 @@ def lib():
         L.ora_fit_subspace.argtypes = [f32p, C.c_int, C.c_int, C.c_int, C.c_double, C.POINTER(OraRandState),
                                        C.POINTER(C.c_int), u8p, f64p]
         L.ora_fit_subspace.restype = C.c_int
+        L.ora_fit_subspace_ex.argtypes = [f32p, C.c_int, C.c_int, C.c_int, C.c_double, C.POINTER(OraRandState),
+                                          C.POINTER(C.c_int), u8p, f64p, C.c_int]
+        L.ora_fit_subspace_ex.restype = C.c_int
         L.ora_subspace_data.argtypes = [f32p, C.c_int, C.c_int, f32p]
         _lib = L
     return _lib
@@ -265,15 +268,17 @@ def subspace_data(traj: np.ndarray) -> np.ndarray:
     return out
 
 
-def fit_subspace(traj: np.ndarray, num_motions: int, sigma: float, st: OraRandState):
+def fit_subspace(traj: np.ndarray, num_motions: int, sigma: float, st: OraRandState, precision: int = 0):
     """OutlierDetector::fitSubspace (outlier_detector.cpp:236-331).  Returns dict(n_outliers,
-    columns (d,), is_outlier (N,), residuals (N,)); n_outliers -1 on bad arguments."""
+    columns (d,), is_outlier (N,), residuals (N,)); n_outliers -1 on bad arguments.  precision 0:
+    double basis + residuals, 1: the reference's float arithmetic shape (ora_fit_subspace_ex)."""
     traj = np.ascontiguousarray(traj, dtype=np.float32)
     N, T = traj.shape[:2]
     d = 4 * num_motions
     cols = np.full(d, -1, np.int32)
     out = np.zeros(max(N, 1), np.uint8)
     res = np.zeros(max(N, 1), np.float64)
-    n = lib().ora_fit_subspace(_p(traj, C.c_float), N, T, num_motions, sigma, C.byref(st),
-                               cols.ctypes.data_as(C.POINTER(C.c_int)), _p(out, C.c_uint8), _p(res, C.c_double))
+    n = lib().ora_fit_subspace_ex(_p(traj, C.c_float), N, T, num_motions, sigma, C.byref(st),
+                                  cols.ctypes.data_as(C.POINTER(C.c_int)), _p(out, C.c_uint8), _p(res, C.c_double),
+                                  int(precision))
     return dict(n_outliers=n, columns=cols, is_outlier=out[:N], residuals=res[:N])

@@ -221,9 +221,11 @@ def test_node_pair_path_matches_oracle(node_exe, tmp_path, mdx, oracle, enc, ski
 
 
 @pytest.mark.gpu
-def test_node_live_path_matches_oracle(node_exe, tmp_path, mdx, oracle):
+@pytest.mark.parametrize("precision", [0, 1])
+def test_node_live_path_matches_oracle(node_exe, tmp_path, mdx, oracle, precision):
     """The node's live branch: every ring frame through calculateOpticalFlowTrajectory, then
-    fitSubspace on the complete trajectories with one rand() stream across frames (seeded)."""
+    fitSubspace on the complete trajectories with one rand() stream across frames (seeded), in
+    double and in the reference's float arithmetic shape (subspace_precision=1)."""
     from motion_detection_amd.formats import write_trajectories
     w, h, ps, nm, sigma, seed = 320, 240, 10, 2, 0.5, 20141105
     a, b, _ = mdx.synth_pair(77, w, h, 3)
@@ -231,7 +233,7 @@ def test_node_live_path_matches_oracle(node_exe, tmp_path, mdx, oracle):
     seq = [a, b, a, b, a, c, d]
     frames = [(x, "rgb8") for x in seq]
     p, out = run_node(node_exe, tmp_path, frames, live_path=True, egomotion=True, num_motions=nm, sigma=sigma,
-                      seed=seed, pixel_step=ps)
+                      seed=seed, pixel_step=ps, subspace_precision=precision)
     assert p.returncode == 0, p.stderr
     ts = 2 * nm + 1
     st = oracle.rand_state(seed)
@@ -244,7 +246,7 @@ def test_node_live_path_matches_oracle(node_exe, tmp_path, mdx, oracle):
         full = np.array(ref["trajectories"], np.float32).reshape(-1, ts, 2)
         assert np.array_equal(r["traj"].view(np.uint32), full.view(np.uint32))
         if len(full):
-            sub = oracle.fit_subspace(full, nm, sigma, st)
+            sub = oracle.fit_subspace(full, nm, sigma, st, precision)
             outl = full[sub["is_outlier"].astype(bool)][:, -2, :]
             assert np.array_equal(r["outliers"], outl.astype(np.float32))
             assert np.array_equal(r["columns"], sub["columns"][sub["columns"] >= 0])

@@ -122,6 +122,25 @@ def test_float32_reference_arithmetic_same_decisions(oracle):
     assert np.array_equal(r["is_outlier"][~near], out[~near])
 
 
+def test_float_mode_is_float_arithmetic(oracle):
+    """precision 1 (explicit float Pnd, float x'(Pnd x), outlier_detector.cpp:272-290): residuals
+    differ from the double mode's only by float rounding -- bounded by a few ulps of |x|^2 per
+    term -- and the decisions agree away from the thresholds."""
+    traj, _ = scene_trajectories(seed=11, noise=0.02)
+    r64 = oracle.fit_subspace(traj, 2, 0.5, oracle.rand_state(5))
+    r32 = oracle.fit_subspace(traj, 2, 0.5, oracle.rand_state(5), precision=1)
+    assert list(r32["columns"]) == list(r64["columns"])
+    data = oracle.subspace_data(traj).reshape(len(traj), -1).astype(np.float64)
+    n = data.shape[1]
+    tol = 8 * n * n * np.finfo(np.float32).eps * (data ** 2).sum(axis=1)
+    diff = np.abs(r32["residuals"] - r64["residuals"])
+    assert np.all(diff <= tol + 1e-6), float((diff / (tol + 1e-6)).max())
+    assert np.any(diff > 0)                       # the float path really ran
+    thr = 0.25 * P99[2]
+    away = np.abs(r64["residuals"] - thr) > tol
+    assert np.array_equal(r32["is_outlier"][away], r64["is_outlier"][away])
+
+
 def test_known_answer_erratic_trajectories_are_outliers(oracle):
     """Two rigid motions (camera + one object) span the 4*num_motions = 8-dim model; erratic
     trajectories (tracking failures) fall outside it and are the outliers."""
@@ -138,11 +157,11 @@ def test_degenerate_arguments(oracle):
 
 
 # ------------------------------------------------------------------------------------ GPU
-def _gpu_vs_oracle(mdx, ctx, oracle, traj, num_motions, sigma, seed):
+def _gpu_vs_oracle(mdx, ctx, oracle, traj, num_motions, sigma, seed, precision=0):
     ps = mdx._lib.MdxRandState()
     mdx.lib().mdx_srand(C.byref(ps), seed)
     g = ctx.fit_subspace(traj, num_motions, sigma, ps)
-    r = oracle.fit_subspace(traj, num_motions, sigma, oracle.rand_state(seed))
+    r = oracle.fit_subspace(traj, num_motions, sigma, oracle.rand_state(seed), precision)
     np.testing.assert_array_equal(g.columns, r["columns"])
     np.testing.assert_array_equal(g.is_outlier, r["is_outlier"])
     np.testing.assert_array_equal(g.residuals.view(np.uint64), r["residuals"].view(np.uint64))
@@ -165,6 +184,19 @@ def _gpu_vs_oracle(mdx, ctx, oracle, traj, num_motions, sigma, seed):
 def test_subspace_gpu_bit_exact(mdx, ctx, oracle, n_bg, n_fg, T, nm, sigma, seed):
     traj, _ = scene_trajectories(n_bg=n_bg, n_fg=n_fg, T=T, seed=seed)
     _gpu_vs_oracle(mdx, ctx, oracle, traj, nm, sigma, seed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_bg,n_fg,T,nm,sigma,seed", [
+    (600, 80, 5, 2, 0.5, 1), (20000, 2000, 5, 2, 0.5, 7), (500, 60, 7, 3, 0.5, 3), (400, 50, 9, 4, 2.0, 4),
+    (3, 0, 5, 2, 0.5, 5),
+])
+def test_subspace_gpu_float_mode_bit_exact(mdx, oracle, n_bg, n_fg, T, nm, sigma, seed):
+    """MDX_SUBSPACE_F32 (the reference's float arithmetic shape): GPU == the oracle's float mode,
+    residual bits included."""
+    traj, _ = scene_trajectories(n_bg=n_bg, n_fg=n_fg, T=T, seed=seed)
+    with mdx.Context(0, 64, 64, 1, subspace_precision=mdx.SUBSPACE_F32) as c:
+        _gpu_vs_oracle(mdx, c, oracle, traj, nm, sigma, seed, precision=1)
 
 
 @pytest.mark.gpu
