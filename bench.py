@@ -599,7 +599,7 @@ def main():
                            iteration=LK_VALU_PER_ELEM_ITER, gradient_sums=LK_VALU_PER_ELEM_A),
                        workload=f"{B} pairs {w}x{h}, pixel_step {ps}, {wk['levels']} levels", **{
                            k: v for k, v in wk.items() if k not in ("valu_lane_instr_per_pair", "levels")})
-        pmc = os.path.join(ROOT, "profiles", "pmc_lk.json")
+        pmc = os.path.join(ROOT, "profiles", "pmc_lk_iter.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 pj = json.load(f)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU box: PMC pass over the default bench step for the LK kernels (k_lk_class, k_lk_A, k_lk_iter):
 # executed VALU / LDS wave-instructions and busy cycles; summarised per step into
-# gpurun_out/pmc_lk/pmc_lk.json by scripts/pmc_lk_to_json.py (copy to profiles/pmc_lk.json).
+# gpurun_out/pmc_lk/pmc_lk.json by scripts/pmc_lk_to_json.py (copy to profiles/pmc_lk_iter.json).
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 S1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS"
 S2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"
