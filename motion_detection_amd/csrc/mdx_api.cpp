@@ -792,7 +792,7 @@ extern "C" int mdx_fit_subspace(mdx_ctx* c, const float* traj, int ntraj, int tr
     const size_t N = (size_t)ntraj;
     int rc;
     if ((rc = ensure(c, c->straj, N * n * 4)) != MDX_OK) return rc;
-    if ((rc = ensure(c, c->sdata, N * n * 4)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->sdata, (N * n + 2) * 4)) != MDX_OK) return rc;   // + the two means
     const size_t qb = std::max((size_t)n * std::max(n - d, 1) * 8, (size_t)n * n * 4);   // F64 basis / F32 Pnd
     if ((rc = ensure(c, c->sq, (size_t)kHyp * qb)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->scnt, kHyp * 4)) != MDX_OK) return rc;

@@ -121,7 +121,7 @@ hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
 // Trajectory subspace RANSAC (fitSubspace): mean-subtracted data, nhyp hypotheses of d columns
 // (cols: [nhyp][d]), winner's residuals / outlier flags; best[0] = winner or -1.  Scratch: data
-// [N][2T] floats, qbuf [nhyp][2T][2T-d] doubles (MDX_SUBSPACE_F32: [nhyp][2T][2T] floats), counts [nhyp].
+// [N][2T] floats + 2 (the means), qbuf [nhyp][2T][2T-d] doubles (MDX_SUBSPACE_F32: [nhyp][2T][2T] floats), counts [nhyp].
 hipError_t launch_subspace(hipStream_t s, const float* traj, int N, int T, int d, const int* cols, int nhyp,
                            double sigma, float* data, double* qbuf, int* counts, double* residuals,
                            uint8_t* is_outlier, int* best, int precision);

@@ -23,15 +23,23 @@ namespace mdx {
 
 constexpr int kMaxSub = 32;   // n = 2 * trajectory length (reference: 10 / 14 / 18 for 2..4 motions)
 
+// acc = acc + v as one v_add_f32 (round to nearest even, like the compiler's).  Written out so
+// the x and y chains stay two scalar chains: the compiler pairs them into one v_pk_add_f32 chain,
+// whose dependent issue is several times slower (k_subspace_prep 306 us -> see DESIGN §7c).
+__device__ __forceinline__ void fadd(float& acc, float v)
+{
+    asm volatile("v_add_f32 %0, %0, %1" : "+v"(acc) : "v"(v));
+}
+
 // meanSubtract.  One workgroup: the row-0 / row-1 sums are sequential float sums (Eigen's
 // row().sum() on a column-major matrix visits the columns in order), staged through LDS in
 // chunks so lane 0's dependent adds read LDS, not HBM.
 __global__ __launch_bounds__(256) void k_subspace_prep(const float* __restrict__ traj, int N, int T,
-                                                        float* __restrict__ data)
+                                                        float* __restrict__ mean)
 {
     constexpr int kChunk = 4096;
     __shared__ __attribute__((aligned(16))) float sx[kChunk], sy[kChunk];
-    __shared__ float s_mean[2];
+    __shared__ float s_ys;
     const int tid = threadIdx.x;
     float xs = 0.f, ys = 0.f;
     for (int base = 0; base < N; base += kChunk) {
@@ -41,51 +49,72 @@ __global__ __launch_bounds__(256) void k_subspace_prep(const float* __restrict__
             sy[i] = traj[(long long)(base + i) * T * 2 + 1];
         }
         __syncthreads();
-        if (tid == 0) {
-            // the reference's order exactly (one float chain per axis); 16 values per axis are
-            // read ahead with ds_read_b128 so the chain waits on the adds, not on LDS latency
+        if (tid == 0 || tid == 64) {
+            // the reference's order exactly: one float chain per axis, the x chain on lane 0 of
+            // wave 0 and the y chain on lane 0 of wave 1 (two SIMDs: a lone wave's dependent adds
+            // issue slowly, so two chains in one wave ran at half this rate).  16 values are read
+            // with ds_read_b128 one block ahead of the adds (software pipelined).
+            const float* sv = tid ? sy : sx;
+            float acc = tid ? ys : xs;
             int i = 0;
-            if (base == 0) { xs = sx[0]; ys = sy[0]; i = 1; }
-            for (; i < m && (i & 3); i++) {
-                xs = xs + sx[i];
-                ys = ys + sy[i];
-            }
-            for (; i + 16 <= m; i += 16) {
-                float4 x4[4], y4[4];
+            if (base == 0) { acc = sv[0]; i = 1; }
+            for (; i < m && (i & 3); i++) fadd(acc, sv[i]);
+            if (i + 16 <= m) {
+                float4 v4[4];
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    x4[k] = reinterpret_cast<const float4*>(sx + i)[k];
-                    y4[k] = reinterpret_cast<const float4*>(sy + i)[k];
+                for (int k = 0; k < 4; k++) v4[k] = reinterpret_cast<const float4*>(sv + i)[k];
+                for (; i + 32 <= m; i += 16) {
+                    float4 n4[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) n4[k] = reinterpret_cast<const float4*>(sv + i + 16)[k];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        fadd(acc, v4[k].x);
+                        fadd(acc, v4[k].y);
+                        fadd(acc, v4[k].z);
+                        fadd(acc, v4[k].w);
+                        v4[k] = n4[k];
+                    }
                 }
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    xs = xs + x4[k].x; ys = ys + y4[k].x;
-                    xs = xs + x4[k].y; ys = ys + y4[k].y;
-                    xs = xs + x4[k].z; ys = ys + y4[k].z;
-                    xs = xs + x4[k].w; ys = ys + y4[k].w;
+                    fadd(acc, v4[k].x);
+                    fadd(acc, v4[k].y);
+                    fadd(acc, v4[k].z);
+                    fadd(acc, v4[k].w);
                 }
+                i += 16;
             }
-            for (; i < m; i++) {
-                xs = xs + sx[i];
-                ys = ys + sy[i];
-            }
+            for (; i < m; i++) fadd(acc, sv[i]);
+            if (tid) ys = acc;
+            else xs = acc;
         }
         __syncthreads();
     }
+    if (tid == 64) s_ys = ys;
+    __syncthreads();
     if (tid == 0) {
-        double xm = (double)xs, ym = (double)ys;
+        double xm = (double)xs, ym = (double)s_ys;
         xm /= N;
         ym /= N;
-        s_mean[0] = (float)xm;
-        s_mean[1] = (float)ym;
+        mean[0] = (float)xm;
+        mean[1] = (float)ym;
     }
-    __syncthreads();
-    const float xc = s_mean[0], yc = s_mean[1];
-    const int n = 2 * T;
-    for (long long e = tid; e < (long long)N * n; e += 256) {
-        const float v = traj[e];
-        const int r = (int)(e % n);
-        data[e] = (r % 2 == 0) ? v - xc : yc - v;
+}
+
+// The centred data, one trajectory per thread over the whole grid (this pass ran inside
+// k_subspace_prep's single workgroup with a 64-bit modulo per element: ~190 us of its 306 us).
+__global__ __launch_bounds__(256) void k_subspace_center(const float* __restrict__ traj, int N, int n,
+                                                          const float* __restrict__ mean, float* __restrict__ data)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const float xc = mean[0], yc = mean[1];
+    const float* t = traj + (long long)i * n;
+    float* d = data + (long long)i * n;
+    for (int r = 0; r < n; r += 2) {
+        d[r] = t[r] - xc;
+        d[r + 1] = yc - t[r + 1];
     }
 }
 
@@ -292,7 +321,10 @@ hipError_t launch_subspace(hipStream_t s, const float* traj, int N, int T, int d
     // chi-square 99% table (outlier_detector.cpp:19-30), indexed by n - d; 0.2 outside 1..10 (:311)
     static const double p99[10] = {0.0, 0.020, 0.115, 0.297, 0.554, 0.872, 1.239, 1.646, 2.088, 2.558};
     const double out_thr = (n - d > 0 && n - d < 10) ? sigma * sigma * p99[n - d] : 0.2;
-    hipLaunchKernelGGL(k_subspace_prep, dim3(1), dim3(256), 0, s, traj, N, T, data);
+    // the two means go to the scratch word after the data ([N * n] floats, then 2)
+    float* mean = data + (size_t)N * n;
+    hipLaunchKernelGGL(k_subspace_prep, dim3(1), dim3(256), 0, s, traj, N, T, mean);
+    hipLaunchKernelGGL(k_subspace_center, dim3((N + 255) / 256), dim3(256), 0, s, traj, N, n, mean, data);
     if (precision == MDX_SUBSPACE_F32) {
         float* pbuf = reinterpret_cast<float*>(qbuf);
         hipLaunchKernelGGL(k_subspace_hyp_f32, dim3(nhyp), dim3(256), 0, s, data, N, n, d, cols, inlier_thr, pbuf,
