@@ -347,7 +347,9 @@ extern "C" int mdx_destroy(mdx_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->pyr1, &c->pyr2, &c->der, &c->fits, &c->in1, &c->in2, &c->np, &c->st,
                       &c->vec, &c->mask, &c->H, &c->Hext, &c->num, &c->bnp, &c->bst,
-                      &c->cls, &c->Abuf, &c->ctab, &c->dbg, &c->csum};
+                      &c->cls, &c->Abuf, &c->ctab, &c->dbg, &c->csum, &c->tin, &c->tcur, &c->tnp, &c->tst,
+                      &c->ttraj, &c->tlen, &c->tvec, &c->tstart, &c->tnum, &c->straj, &c->sdata, &c->sq,
+                      &c->scnt, &c->scols, &c->sres, &c->sout, &c->sbest};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (c->ev) {
