@@ -147,6 +147,7 @@ __device__ TileInfo tile_info(const double* M, int x0, int y0, int w, int yend, 
 }
 
 // LDS pointers stay 32-bit (address space 3) through the inlined helpers
+typedef __attribute__((address_space(3))) void* lds_ptr;
 typedef __attribute__((address_space(3))) const uint8_t lds_u8;
 typedef __attribute__((address_space(3))) const uint32_t lds_u32;
 typedef double d2v __attribute__((ext_vector_type(2)));
@@ -227,11 +228,6 @@ __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t sr
         __builtin_amdgcn_raw_buffer_store_b32(out, mrs, (int)moff, i * ms, 0);
     }
 }
-
-// staging: rows per pass and ceil(2^16 / nch) for nch = 1..16 chunks per footprint row
-__constant__ int kRowsPerPass[17] = {0, 256, 128, 85, 64, 51, 42, 36, 32, 28, 25, 23, 21, 19, 18, 17, 16};
-__constant__ uint32_t kInvChunks[17] = {0,     65536, 32768, 21846, 16384, 13108, 10923, 9363, 8192,
-                                        7282,  6554,  5958,  5462,  5042,  4682,  4370,  4096};
 
 // footprint chunks that cross the image's left / right edge: byte by byte, 0 outside (kept out of
 // line so its per-byte bounds are not computed on the interior path)
@@ -334,27 +330,30 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
         s_xy[r][b][1] = M[3] * xb + M[4] * y + M[5];
     }
     {
-        // lane -> (row, 16-B chunk) of the footprint without an integer division: ro = tid / nch
-        // as a multiply by ceil(2^16 / nch) (exact for tid < 4096)
+        // LDS-DMA (buffer_load ... lds): one wave instruction fills 4 staged rows (lane L -> row
+        // 4q + L/16, chunk L%16 at LDS byte 16L of the 1-KiB group), straight from memory to LDS.
+        // Chunks past the footprint's width, and rows above / below the image, get an
+        // out-of-range offset and land as zeros (BORDER_CONSTANT); chunks crossing the image's
+        // left / right edge are rewritten byte by byte once the DMA has landed.
         const int nch = (t.sw + 15) >> 4;                 // <= kSP / 16
-        const int rpp = kRowsPerPass[nch];                // 256 / nch rows per pass
-        const int ro = (int)(((uint32_t)tid * kInvChunks[nch]) >> 16), ch = tid - ro * nch;
-        const int sx = t.sxa + 16 * ch;
-        if (ro < rpp) {
-            if (sx >= 0 && sx + 16 <= w) {
-                // whole chunks inside the row: buffer loads, rows above / below the image fall
-                // outside the descriptor and read 0 (BORDER_CONSTANT)
-                const __amdgpu_buffer_rsrc_t srs = buf_rsrc(src, (long long)h * g1_pitch);
-                uint32_t off = (uint32_t)((t.sya + ro) * g1_pitch + sx);
-                const uint32_t step = (uint32_t)(rpp * g1_pitch);
-                for (int r = ro; r < t.sh; r += rpp, off += step) {
-                    const v4u v = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)off, 0, 0);
-                    *reinterpret_cast<uint4*>(&s_src[r * kSP + 16 * ch]) = make_uint4(v.x, v.y, v.z, v.w);
-                }
-            } else {
-                stage_edge_chunks(src, g1_pitch, w, h, t.sya, sx, ro, rpp, t.sh, &s_src[16 * ch]);
-            }
+        const __amdgpu_buffer_rsrc_t srs = buf_rsrc(src, (long long)h * g1_pitch);
+        const int ch = lane & 15, sx = t.sxa + 16 * ch;
+        const bool inner = ch < nch && sx >= 0 && sx + 16 <= w;
+        for (int q = wave; 4 * q < t.sh; q += 4) {
+            const int r = 4 * q + (lane >> 4);
+            const int sy = t.sya + r;
+            const uint32_t off = (inner && r < t.sh && (unsigned)sy < (unsigned)h) ? (uint32_t)(sy * g1_pitch + sx)
+                                                                                  : 0x80000000u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, (lds_ptr)&s_src[4 * q * kSP], 16, (int)off, 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0x0F70);               // vmcnt(0): this wave's DMA has landed
+        __builtin_amdgcn_sched_barrier(0);
+        if (ch < nch && !inner)
+            for (int q = wave; 4 * q < t.sh; q += 4) {
+                const int r = 4 * q + (lane >> 4);
+                if (r < t.sh) stage_edge_chunks(src, g1_pitch, w, h, t.sya, sx, r, t.sh, t.sh, &s_src[16 * ch]);
+            }
     }
     __syncthreads();
 
