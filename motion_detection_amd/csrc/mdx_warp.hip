@@ -17,9 +17,9 @@
 // wave w owns the 4 columns x0 + 4*(l & 31) .. +3 of rows y0 + 8i + 2w + (l >> 5), i = 0..7: a
 // half-wave is one tile row, so gray2 loads / mask stores are dwords, 128 contiguous bytes.
 //   * Footprint: X, Y are monotone in x and y inside a reference block for affine M, so the eight
-//     block corners bound the tile's taps exactly.  It is staged once into LDS as raw bytes
-//     (16-B loads, ds_write_b128), zero outside the image (= BORDER_CONSTANT 0 per tap), at a row
-//     pitch of 256 B.
+//     block corners bound the tile's taps exactly.  It is staged once into LDS as raw bytes by
+//     LDS-DMA (buffer_load ... lds, 16 B per lane, 4 staged rows per wave instruction), zero
+//     outside the image (= BORDER_CONSTANT 0 per tap), at a row pitch of 256 B.
 //   * Coordinates, per pixel: one FP64 add (per-row X0 from an LDS table + per-column M0*x1 in
 //     registers) and one FMA with the magic constant 1.5*2^52 - 32*origin per axis, whose low word
 //     is cvRound(32*(...)) - 32*origin (round-half-even, exact for |X| < 2^30, checked per tile).
