@@ -1122,22 +1122,31 @@ hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const u
     return hipGetLastError();
 }
 
-// k_front's band height: 4 destination rows while a band's LDS fits 32 KB (5-6 bands per CU),
-// else 2.  At 1080p x 32 one frame side of gray + pad + level 1 takes 44 us against 56 with 8 rows
-// and 107 for k_gray_pad + k_pyrdown (scripts/micro/front_bench.hip).
+// k_front's band height: 4 destination rows at 1080p (27 KB of LDS, 5-6 bands per CU): one frame
+// side of gray + pad + level 1 takes 44 us there against 56 with 8 rows and 107 for the earlier
+// k_gray_pad + k_pyrdown (scripts/micro/front_bench.hip).
 static hipError_t launch_front_bands(hipStream_t s, FrontArgs& a, int mode)
 {
-    const bool wide = (2 * 4 + 3) * a.lp + 4 * a.lp1 > 32 * 1024;
-    const int rb = wide ? 2 : 4;
+    // the band height: 4 destination rows while a band's LDS fits 32 KB, else 2 (8K frames: 62 KB),
+    // else 1; beyond 64 KB (rows wider than ~8.7K px at RB = 1) the launch asks for the larger
+    // dynamic LDS explicitly (up to the CU's 160 KB)
+    auto lds_of = [&](int rb) { return (size_t)(2 * rb + 3) * a.lp + (size_t)rb * a.lp1; };
+    const int rb = lds_of(4) <= 32 * 1024 ? 4 : lds_of(2) <= 64 * 1024 ? 2 : 1;
+    const size_t lds = lds_of(rb);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;   // rows wider than ~31K px
     a.nbands = (a.L1.h + rb - 1) / rb;
     const dim3 grid((unsigned)(a.nbands * a.nz));
-    const size_t lds = (size_t)(2 * rb + 3) * a.lp + (size_t)rb * a.lp1;
-#define MDX_FRONT_CASE(M)                                                              \
-    if (mode == M) {                                                                   \
-        if (wide) hipLaunchKernelGGL((k_front<2, M>), grid, dim3(256), lds, s, a);     \
-        else hipLaunchKernelGGL((k_front<4, M>), grid, dim3(256), lds, s, a);          \
+#define MDX_FRONT_CASE(M, R)                                                                             \
+    if (mode == M && rb == R) {                                                                          \
+        if (lds > 64 * 1024)                                                                             \
+            if (hipError_t e = hipFuncSetAttribute((const void*)k_front<R, M>,                           \
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) \
+                return e;                                                                                \
+        hipLaunchKernelGGL((k_front<R, M>), grid, dim3(256), lds, s, a);                                 \
     }
-    MDX_FRONT_CASE(0) MDX_FRONT_CASE(1) MDX_FRONT_CASE(2)
+    MDX_FRONT_CASE(0, 4) MDX_FRONT_CASE(0, 2) MDX_FRONT_CASE(0, 1)
+    MDX_FRONT_CASE(1, 4) MDX_FRONT_CASE(1, 2) MDX_FRONT_CASE(1, 1)
+    MDX_FRONT_CASE(2, 4) MDX_FRONT_CASE(2, 2) MDX_FRONT_CASE(2, 1)
 #undef MDX_FRONT_CASE
     return hipGetLastError();
 }

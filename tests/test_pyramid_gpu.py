@@ -1,10 +1,10 @@
 """GPU parity of the front end alone: every padded pyramid level the HIP path leaves in HBM
-(k_front = gray + pad + level-1 pyrDown, then k_pyrdown for the coarser levels) equals the
-oracle's buildOpticalFlowPyramid images byte for byte, borders included (lkpyramid.cpp:
+(k_front = gray + pad + level-1 pyrDown, then k_front's level mode for the coarser levels) equals
+the oracle's buildOpticalFlowPyramid images byte for byte, borders included (lkpyramid.cpp:
 buildOpticalFlowPyramid with BORDER_REFLECT_101, withDerivatives; reference call at
 optical_flow_calculator.cpp:71).  Both the split-frame launch of the pair path (first frames,
-then second frames) and the both-frames launch of the trajectory path are covered; the 4K case
-takes k_front's narrow-band variant (4 level-1 rows per workgroup).
+then second frames) and the both-frames launch of the trajectory path are covered; the band
+heights 4 (1080p), 2 (4K level 0) and 1 (a 12K-wide row, > 64 KB of LDS) all run.
 """
 import numpy as np
 import pytest
@@ -68,6 +68,7 @@ CASES = [
     (1920, 1080, 1, 6),
     (1921, 1081, 3, 7),
     (3840, 2160, 1, 8),
+    (12000, 100, 1, 11),      # a 12K-wide row: one level-1 row per band, > 64 KB of LDS requested
 ]
 
 
