@@ -115,8 +115,8 @@ __global__ __launch_bounds__(256) void k_gray_pad(const uint8_t* __restrict__ in
 // Frame mode (MODE 0/1): gray + level-0 padding + level 1 in one pass.  A workgroup owns RB level-1
 // core rows [Y0, Y0+RB) and the level-0 core rows [2 Y0, 2 Y0 + 2 RB):
 //   1  stage level-0 padded rows 2 Y0 - 2 .. 2 Y0 + 2 RB (reflect-101 in both directions, gray of
-//      rgb8 on the fly) in LDS: interior 16-B chunks by vector loads, K per thread in flight, the
-//      border bytes one per lane;
+//      rgb8 on the fly) in LDS: interior 16-B chunks by LDS-DMA (mono8; rgb8/bgr8 by vector loads,
+//      K per thread in flight, and the gray conversion), the border bytes one per lane;
 //   2  write the band's level-0 rows, and every border row that mirrors one of them, from LDS;
 //   3a level-1 core rows into an LDS row buffer: a thread owns 4 level-1 columns and walks down
 //      the band, each staged row's horizontal 5-tap sums (two chained v_dot4_u32_u8 per pixel)
@@ -126,10 +126,10 @@ __global__ __launch_bounds__(256) void k_gray_pad(const uint8_t* __restrict__ in
 // Level 0 thus crosses HBM once (written) instead of three times (written, read back by a
 // separate pyrDown); source halo rows are shared with the neighbouring band through L2
 // (consecutive bands go to the same XCD).  Level mode (MODE 2) runs the same band schedule from
-// an already padded level to the next (phase 1 = plain 16-B copies of the padded source rows, no
+// an already padded level to the next (phase 1 = LDS-DMA copies of the padded source rows, no
 // phase 2).  Measured at 1080p x 32, one frame side (scripts/micro/front_bench.hip): levels 0-1
-// 44 us (3.7 TB/s of 162 MB) and levels 2-4 32 us, against 107 + 42 us for the earlier
-// k_gray_pad + per-level pyrDown kernels.  Per-pixel reflect-101 gathers in the hot loops cost
+// 40 us (4.0 TB/s of 162 MB) and levels 2-4 20 us, against 107 + 42 us for the earlier
+// k_gray_pad + per-level pyrDown kernels (44 + 30 us with vector loads instead of LDS-DMA).  Per-pixel reflect-101 gathers in the hot loops cost
 // ~2-5 us per workgroup (measured): borders are built byte-per-lane from data already in LDS.
 struct FrontArgs {
     const uint8_t* in1;
@@ -163,6 +163,8 @@ __device__ __forceinline__ int fdiv(int a, int b, float rb)
     else if ((q + 1) * b <= a) q++;
     return q;
 }
+
+typedef __attribute__((address_space(3))) void* front_lds_ptr;
 
 // MODE 0: mono8 frames, 1: rgb8/bgr8 frames (gray + pad + level 1, as above); MODE 2: one
 // pyramid level L -> L+1 (a.L0 = source level, already padded in the slab, a.L1 = destination):
@@ -213,35 +215,42 @@ __global__ __launch_bounds__(256) void k_front(FrontArgs a)
     // or 48-B (rgb8/bgr8) loads, K per thread in flight; the few border chunks go through the
     // per-pixel reflect-101 path in a loop of their own.
     const int nc0 = a.nchunk0;
-    if constexpr (!FRAME) {
-        // padded source rows r0-2 .. r0+2RB of level a.L0, chunks 1 .. nc0, K loads in flight
-        const uint8_t* lvl = slab + a.L0.img_off + (long long)kPad * a.L0.pitch;
-        const float rc = 1.f / (float)nc0;
-        const int n1 = NR * nc0;
-        for (int base = 0; base < n1; base += 256 * K) {
-            uint4 v[K];
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                const int item = base + k * 256 + tid;
-                if (item < n1) {
-                    const int i = fdiv(item, nc0, rc), c = 1 + item - i * nc0;
-                    v[k] = *reinterpret_cast<const uint4*>(lvl + (long long)(r0 - 2 + i) * a.L0.pitch + 16 * c);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                const int item = base + k * 256 + tid;
-                if (item >= n1) continue;
-                const int i = fdiv(item, nc0, rc), c = 1 + item - i * nc0;
-                *reinterpret_cast<uint4*>(lds + i * a.lp + 16 * c) = v[k];
-            }
-        }
-    }
     const int cA = kXOff / 16;
     int cB = a.aligned ? (w + kXOff - 16) / 16 : cA - 1;
     if (cB < cA) cB = cA - 1;
     const int ni = cB - cA + 1;
-    if (FRAME && ni > 0) {
+    if constexpr (MODE != 1) {
+        // mono8 frames and level mode: LDS-DMA (buffer_load ... lds) straight into the staged rows.
+        // Flat 16-B slot f is row f / (nc0 + 1), chunk f % (nc0 + 1) (LDS byte 16 f); one wave
+        // instruction fills 64 consecutive slots.  Frame mode loads the interior chunks [cA, cB]
+        // and leaves the rest to the border-byte pass below (an out-of-range offset lands zeros
+        // there first); level mode copies whole padded rows.
+        const int spr = nc0 + 1, nslot = NR * spr;
+        const float rs = 1.f / (float)spr;
+        const uint8_t* rbase = FRAME ? src : slab + a.L0.img_off;
+        const long long rbytes = FRAME ? (long long)h * a.stride : (long long)a.L0.rows * a.L0.pitch;
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(rbase), (short)0, (int)min(rbytes, (long long)0x7fffffff), 0x00020000);
+        const int wave = tid >> 6, wl = tid & 63;
+        for (int b0 = 64 * wave; b0 < nslot; b0 += 256) {
+            const int f = b0 + wl;
+            if (f < nslot) {
+                const int i = fdiv(f, spr, rs), c = f - i * spr;
+                uint32_t off = 0x80000000u;
+                if constexpr (FRAME) {
+                    if (c >= cA && c <= cB) off = (uint32_t)(r101s(r0 - 2 + i, h) * a.stride + 16 * c - kXOff);
+                } else {
+                    off = (uint32_t)((r0 - 2 + i + kPad) * a.L0.pitch + 16 * c);
+                }
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (front_lds_ptr)(lds + 16 * b0), 16, (int)off, 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0x0F70);               // vmcnt(0): this wave's DMA has landed
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (FRAME) __syncthreads();             // before any wave rewrites border slots
+    }
+    if (MODE == 1 && ni > 0) {
         const float rci = 1.f / (float)ni;
         const int n1 = NR * ni;
         for (int base = 0; base < n1; base += 256 * K) {
