@@ -277,10 +277,11 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
                                              int* __restrict__ qctr, int level, int ngroups)
 {
     using Sh = LkShape<G, UW>;
-    constexpr int LPS = Sh::LPS, S = Sh::S, NP = Sh::NP;
-    constexpr int UWP = 2 * LPS * NP;                             // staged pairs per slot row
+    constexpr int LPS = Sh::LPS, S = Sh::S, ND = Sh::ND;
+    constexpr int NB = 3;                                          // row images: 2 rows in flight ahead
     constexpr float FLT_SCALE = 1.f / (1 << 20);
-    __shared__ __attribute__((aligned(16))) uint32_t lds[2][S][UWP];
+    // [buf][slot][UW][D, C]: the wave's union row image, filled by LDS-DMA like k_lk_iter's
+    __shared__ __attribute__((aligned(16))) uint32_t img[NB][ND * 256];
 
     const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
     const int nw = gridDim.x;
@@ -295,45 +296,47 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
 
     const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cls + (long long)pair * a.plan.bytes_per_pair, a.plan.bytes_per_pair);
     const uint32_t rowb = (uint32_t)C.PW * 8;
-    uint32_t roff = q.ubase + (uint32_t)q.v0 * rowb + 16u * sl;
-    const uint32_t* lD0 = &lds[0][slot][q.off + k];
-    // rows are loaded PF ahead (this kernel has few waves' worth of VALU work to hide latency)
-    constexpr int PF = 4;
-    uint4 rq[PF][NP];
-    // whole loads: the staged row runs up to UWP >= UW pairs (the tail is never read by a chain;
-    // past the plane row it is the next row's data, past the slab the descriptor returns zero)
-    auto gload = [&](uint4 (&rd)[NP]) {
+    // lane L of piece c fills image bytes 1024c + 16L: slot sp's union bytes wb (past the image:
+    // an out-of-range offset, zeros)
+    uint32_t uoff[ND];
+    {
+        const uint32_t mine = q.ubase + (uint32_t)q.v0 * rowb;
 #pragma unroll
-        for (int c = 0; c < NP; c++) {
-            const v4u t = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)(roff + 16u * LPS * c), 0, 0);
-            rd[c] = make_uint4(t.x, t.y, t.z, t.w);
+        for (int c = 0; c < ND; c++) {
+            const int P = 1024 * c + 16 * lane;
+            const int sp = P / (8 * UW), wb = P % (8 * UW);
+            const uint32_t src = (uint32_t)__shfl((int)mine, (sp < S ? sp : 0) * LPS) + (uint32_t)wb;
+            uoff[c] = sp < S ? src : 0x80000000u;
         }
-        roff += rowb;
-    };
-    auto lstore = [&](int buf, const uint4 (&rd)[NP]) {   // the D word of each (D, C) pair
+    }
+    auto dma = [&](int b) {
 #pragma unroll
-        for (int c = 0; c < NP; c++)
-            *reinterpret_cast<uint2*>(&lds[buf][slot][2 * (LPS * c + sl)]) = make_uint2(rd[c].x, rd[c].z);
+        for (int c = 0; c < ND; c++) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)&img[b][256 * c], 16, (int)uoff[c], 0, 0, 0);
+            uoff[c] += rowb;
+        }
     };
+    lds_u2v* lE = (lds_u2v*)&img[0][2 * (slot * UW + q.off + k)];
 
     // lane k owns SSE lane k (columns 4g+k), rows in order; ((P0+P1)+P2)+P3 across the quad
     f2 sd = {0.f, 0.f};
     float s12 = 0.f;
-    {
-        uint4 r0[NP];
-        gload(r0);
-#pragma unroll
-        for (int i = 0; i < PF; i++) gload(rq[i]);
-        lstore(0, r0);
-    }
-    wave_lds_fence();
+    dma(0);
+    dma(1);
 #pragma unroll
     for (int y = 0; y < kWin; y++) {
-        const int buf = y & 1;
-        const uint32_t* ld = lD0 + buf * (S * UWP);
+        const int buf = y % NB;
+        // row y has landed once at most the next row's ND pieces are outstanding
+        __builtin_amdgcn_sched_barrier(0);
+        if (y + 1 < kWin) __builtin_amdgcn_s_waitcnt(0x0F70 | ND);
+        else __builtin_amdgcn_s_waitcnt(0x0F70);
+        __builtin_amdgcn_sched_barrier(0);
+        // row y+2 into the image row y-1 used (its reads were consumed last iteration)
+        if (y + 2 < kWin) dma((y + 2) % NB);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int gi = 0; gi < 10; gi++) {
-            const uint32_t d = ld[4 * gi];
+            const uint32_t d = lE[buf * (ND * 128) + 4 * gi].x;   // the D word of pair q.off + k + 4 gi
             const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
             // the reference rounds each product to float, then adds (_mm_mul_ps, _mm_add_ps).
             // |Ix|, |Iy| <= 4080 (Scharr of u8, interpolated), so every product is below 2^24 and
@@ -341,11 +344,6 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
             sd = __builtin_elementwise_fma(f, f, sd);      // (Ix*Ix, Iy*Iy)
             s12 = __builtin_fmaf(f.x, f.y, s12);           // Ix*Iy
         }
-        if (y + 1 < kWin) {
-            lstore(buf ^ 1, rq[y % PF]);     // row y+1
-            if (y + 1 + PF < kWin) gload(rq[y % PF]);
-        }
-        wave_lds_fence();
     }
     const float a11 = ((quad_bcast<0>(sd.x) + quad_bcast<1>(sd.x)) + quad_bcast<2>(sd.x)) + quad_bcast<3>(sd.x);
     const float a12 = ((quad_bcast<0>(s12) + quad_bcast<1>(s12)) + quad_bcast<2>(s12)) + quad_bcast<3>(s12);
