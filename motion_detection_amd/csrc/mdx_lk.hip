@@ -278,7 +278,7 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
 {
     using Sh = LkShape<G, UW>;
     constexpr int LPS = Sh::LPS, S = Sh::S, ND = Sh::ND;
-    constexpr int NB = 3;                                          // row images: 2 rows in flight ahead
+    constexpr int NB = 3;                                          // row images: NB - 1 rows in flight ahead
     constexpr float FLT_SCALE = 1.f / (1 << 20);
     // [buf][slot][UW][D, C]: the wave's union row image, filled by LDS-DMA like k_lk_iter's
     __shared__ __attribute__((aligned(16))) uint32_t img[NB][ND * 256];
@@ -321,18 +321,22 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
     // lane k owns SSE lane k (columns 4g+k), rows in order; ((P0+P1)+P2)+P3 across the quad
     f2 sd = {0.f, 0.f};
     float s12 = 0.f;
-    dma(0);
-    dma(1);
+    constexpr int PF = NB - 1;                                     // rows in flight ahead
+#pragma unroll
+    for (int y = 0; y < PF; y++) dma(y);
 #pragma unroll
     for (int y = 0; y < kWin; y++) {
         const int buf = y % NB;
-        // row y has landed once at most the next row's ND pieces are outstanding
+        // row y has landed once at most the later rows' pieces are outstanding
         __builtin_amdgcn_sched_barrier(0);
-        if (y + 1 < kWin) __builtin_amdgcn_s_waitcnt(0x0F70 | ND);
+        const int later = (y + PF - 1 < kWin - 1 ? y + PF - 1 : kWin - 1) - y;
+        if (later >= 3) __builtin_amdgcn_s_waitcnt(0x0F70 | (3 * ND));
+        else if (later == 2) __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * ND));
+        else if (later == 1) __builtin_amdgcn_s_waitcnt(0x0F70 | ND);
         else __builtin_amdgcn_s_waitcnt(0x0F70);
         __builtin_amdgcn_sched_barrier(0);
-        // row y+2 into the image row y-1 used (its reads were consumed last iteration)
-        if (y + 2 < kWin) dma((y + 2) % NB);
+        // row y+PF into the image row y-1 used (its reads were consumed last iteration)
+        if (y + PF < kWin) dma((y + PF) % NB);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int gi = 0; gi < 10; gi++) {
