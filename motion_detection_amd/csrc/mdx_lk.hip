@@ -54,6 +54,7 @@ typedef short s2 __attribute__((ext_vector_type(2)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 // 4-B aligned 8-byte loads (global_load_dwordx2 at dword-aligned addresses)
 struct __attribute__((aligned(4))) u2a4 { uint32_t x, y; };
+struct __attribute__((aligned(4))) u3a4 { uint32_t x, y, z; };
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v3u __attribute__((ext_vector_type(3)));
 // raw buffer descriptor over [base, base + bytes) (cdna_hip_programming.md T8: built from
@@ -199,6 +200,95 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
     uint4* o = reinterpret_cast<uint4*>(base) + ((long long)v * C.PW + 4 * j) / 2;
     o[0] = make_uint4(dv[0], (uint32_t)cv[0], dv[1], (uint32_t)cv[1]);
     o[1] = make_uint4(dv[2], (uint32_t)cv[2], dv[3], (uint32_t)cv[3]);
+}
+
+// Levels with at most 4 residue classes (the finest ones, whose Scharr planes are the largest):
+// the same elements, with the Scharr derivatives computed here from the padded level image instead
+// of read back from k_scharr's planes (lkpyramid.cpp calcSharrDeriv: t0 = 3(a+c)+10b, t1 = c-a,
+// Ix = t0[x+1]-t0[x-1], Iy = 3(t1[x-1]+t1[x+1])+10 t1[x]; the padded level's reflect-101 rows and
+// columns are OpenCV's neighbour clamping; 0 outside the level, the derivative planes' CONSTANT
+// border).  One thread serves every class of its pair from one set of row loads, and the level's
+// k_scharr launch (its plane writes and their reads) is skipped.
+__device__ __forceinline__ int u8_at(const uint32_t (&w)[3], int b) { return (int)((w[b >> 2] >> (8 * (b & 3))) & 255u); }
+
+__global__ __launch_bounds__(256) void k_lk_class_fused(const uint8_t* __restrict__ pyr1, uint8_t* __restrict__ cls_out,
+                                                        LkClassArgs a)
+{
+    const int level = a.level;
+    const ClassLevel& C = a.plan.lv[level];
+    const int nclass = C.nrx * C.nry;                // <= 4 (host)
+    const int pair = blockIdx.z;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int v = C.vlo + blockIdx.y;
+    if (4 * j >= a.g.lv[level].w + 2 * kPad || v >= C.UH) return;
+    const Level L = a.g.lv[level];
+    const float scale = (float)(1. / (1 << level));
+    const uint8_t* I = pyr1 + (long long)pair * a.g.img_bytes + L.img_off + L.core();
+    const int y = v - kPad;
+    const int p = L.pitch;
+    const int x0 = 4 * j - kPad;
+    const bool inside = y < L.h + kPad - 1 && x0 < L.w + kPad - 1;
+    // image rows y-1 .. y+2, bytes x0-4 .. x0+7 (3 aligned dwords each); rows outside the padded
+    // level are never used (their derivatives are 0) and read row y instead
+    uint32_t rw[4][3];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int yy = y - 1 + r;
+        const int ys = (yy < -kPad || yy >= L.h + kPad) ? y : yy;
+        const u3a4 t = *reinterpret_cast<const u3a4*>(I + (long long)ys * p + x0 - 4);
+        rw[r][0] = t.x; rw[r][1] = t.y; rw[r][2] = t.z;
+    }
+    // derivative words at columns x0 .. x0+4 of rows y, y+1 (k_lk_class's dw)
+    uint32_t dw[2][5];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const int yy = y + r;
+#pragma unroll
+        for (int c = 0; c < 5; c++) {
+            const int x = x0 + c;
+            uint32_t d = 0;
+            if (yy >= 0 && yy < L.h && x >= 0 && x < L.w) {
+                const int bm = 3 + c, bc = 4 + c, bp = 5 + c;          // bytes x-1, x, x+1
+                const int t0m = (u8_at(rw[r], bm) + u8_at(rw[r + 2], bm)) * 3 + u8_at(rw[r + 1], bm) * 10;
+                const int t0p = (u8_at(rw[r], bp) + u8_at(rw[r + 2], bp)) * 3 + u8_at(rw[r + 1], bp) * 10;
+                const int t1m = u8_at(rw[r + 2], bm) - u8_at(rw[r], bm), t1c = u8_at(rw[r + 2], bc) - u8_at(rw[r], bc);
+                const int t1p = u8_at(rw[r + 2], bp) - u8_at(rw[r], bp);
+                const int ix = t0p - t0m, iy = (t1m + t1p) * 3 + t1c * 10;
+                d = (uint32_t)(uint16_t)(int16_t)ix | ((uint32_t)(uint16_t)(int16_t)iy << 16);
+            }
+            dw[r][c] = d;
+        }
+    }
+    // the image bytes of rows y, y+1 at columns x0 .. x0+4 (k_lk_class's ib): bytes 4 .. 8
+    for (int cls = 0; cls < nclass; cls++) {
+        const int rx = residue_of(a.rlist, level, 0, cls % C.nrx), ry = residue_of(a.rlist, level, 1, cls / C.nrx);
+        const float ppx = (float)rx * scale - 19.5f, ppy = (float)ry * scale - 19.5f;
+        const float fa = ppx - floorf(ppx), fb = ppy - floorf(ppy);
+        int w00, w01, w10, w11;
+        lk_weights(fa, fb, w00, w01, w10, w11);
+        uint32_t dv[4] = {0, 0, 0, 0};
+        int cv[4] = {256, 256, 256, 256};
+        if (inside) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (x0 + q >= L.w + kPad - 1) continue;
+                const int i00 = u8_at(rw[1], 4 + q), i01 = u8_at(rw[1], 5 + q);
+                const int i10 = u8_at(rw[2], 4 + q), i11 = u8_at(rw[2], 5 + q);
+                const int ival = (i00 * w00 + i01 * w01 + i10 * w10 + i11 * w11 + 256) >> 9;
+                const uint32_t d00 = dw[0][q], d01 = dw[0][q + 1], d10 = dw[1][q], d11 = dw[1][q + 1];
+                const int ixv = ((int)(int16_t)d00 * w00 + (int)(int16_t)d01 * w01 + (int)(int16_t)d10 * w10 +
+                                 (int)(int16_t)d11 * w11 + 8192) >> 14;
+                const int iyv = (((int)d00 >> 16) * w00 + ((int)d01 >> 16) * w01 + ((int)d10 >> 16) * w10 +
+                                 ((int)d11 >> 16) * w11 + 8192) >> 14;
+                dv[q] = ((uint32_t)ixv & 0xffffu) | ((uint32_t)iyv << 16);
+                cv[q] = 256 - 512 * ival;
+            }
+        }
+        uint8_t* base = cls_out + (long long)pair * a.plan.bytes_per_pair + C.off + (long long)cls * C.class_bytes;
+        uint4* o = reinterpret_cast<uint4*>(base) + ((long long)v * C.PW + 4 * j) / 2;
+        o[0] = make_uint4(dv[0], (uint32_t)cv[0], dv[1], (uint32_t)cv[1]);
+        o[1] = make_uint4(dv[2], (uint32_t)cv[2], dv[3], (uint32_t)cv[3]);
+    }
 }
 
 // ------------------------------------------------------------------ one pyramid level
@@ -716,11 +806,17 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             ca.plan = a.plan;
             ca.rlist = a.rlist;
             ca.level = l;
-            const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.vhi - C.vlo, nb * C.nrx * C.nry);
-            // this level's Scharr planes (the caller left them to us): on the aux stream, so they
-            // too run while the coarser levels iterate
-            if (hipError_t e = launch_scharr(sa, nb, b.pyr1, const_cast<uint32_t*>(b.der), a.g, l)) return e;
-            hipLaunchKernelGGL(k_lk_class, grid, dim3(64), 0, sa, b.pyr1, b.der, bcls, ca);
+            if (C.nrx * C.nry <= 4) {
+                // the finest levels: derivatives computed inside the class kernel, no Scharr planes
+                const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.vhi - C.vlo, nb);
+                hipLaunchKernelGGL(k_lk_class_fused, grid, dim3(64), 0, sa, b.pyr1, bcls, ca);
+            } else {
+                const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.vhi - C.vlo, nb * C.nrx * C.nry);
+                // this level's Scharr planes (the caller left them to us): on the aux stream, so
+                // they too run while the coarser levels iterate
+                if (hipError_t e = launch_scharr(sa, nb, b.pyr1, const_cast<uint32_t*>(b.der), a.g, l)) return e;
+                hipLaunchKernelGGL(k_lk_class, grid, dim3(64), 0, sa, b.pyr1, b.der, bcls, ca);
+            }
             float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             const int G = C.G, UW = C.UW;
             switch (G * 1000 + UW) {
