@@ -167,6 +167,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, lon
 // 64*(32-f, f)); src_base is the staged footprint.  g2 / mask go through buffer descriptors whose
 // per-lane offsets are out of range for idle lanes; ROWCHK (partial tiles) sends rows past the
 // band to row r0's coordinates so every tap stays inside the footprint.
+// Cache policy of the streamed operands: gray2 is read once and the mask written once, so both go
+// non-temporal (nt).  The staged footprint keeps the default policy: adjacent tiles share its margin
+// lines in L2.  4K x 32 launch, alternating on one box: 216-224 us with nt on gray2 + mask, 233-235
+// without, 230-234 with nt on the footprint too, 222-224 with nt on the mask only; on a second box
+// 211-220 with nt against 223-229 without.
+constexpr int kCpStream = 2;   // buffer aux bit 1 = nt
 template <bool POW2, bool ROWCHK>
 __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t src_base, int nvalid,
                                           __amdgpu_buffer_rsrc_t g2rs, uint32_t g2off, int g2s,
@@ -175,7 +181,7 @@ __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t sr
 {
     uint32_t G[kTH / 8];
 #pragma unroll
-    for (int i = 0; i < kTH / 8; i++) G[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * g2s, 0);
+    for (int i = 0; i < kTH / 8; i++) G[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * g2s, kCpStream);
 #pragma unroll
     for (int i = 0; i < kTH / 8; i++) {
         const d2v xy = xyp[ROWCHK ? (i < nvalid ? 16 * i : 0) : 16 * i];   // rows are 2 blocks x 16 B apart
@@ -225,7 +231,7 @@ __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t sr
         }
         // v_perm selectors 9 / 11 replicate bit 31 of src1 / src0: 0xff or 0x00 bytes
         const uint32_t out = __builtin_amdgcn_perm(e[1], e[0], 0x0c0c0b09u) | __builtin_amdgcn_perm(e[3], e[2], 0x0b090c0cu);
-        __builtin_amdgcn_raw_buffer_store_b32(out, mrs, (int)moff, i * ms, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(out, mrs, (int)moff, i * ms, kCpStream);
     }
 }
 
