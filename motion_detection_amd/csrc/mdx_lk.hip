@@ -132,6 +132,19 @@ __device__ __forceinline__ int xcd_remap(int b, int total)
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+// Class-plane stores go non-temporal: a level's planes (tens of MB per batch) do not fit in L2 and
+// are re-read from HBM/MALL by k_lk_A and k_lk_iter anyway, and these kernels run on the aux stream
+// beside the coarser levels' iterations, whose row re-reads keep their L2 lines this way.  Whole
+// path, alternating on two boxes: 7129 / 7106 vs 7071 / 7046 Mpx/s (6 runs each, 5 of 6 pairs ahead).
+__device__ __forceinline__ void cls_store(uint4* o, const uint32_t (&dv)[4], const int (&cv)[4])
+{
+    typedef unsigned v4nt __attribute__((ext_vector_type(4)));
+    const uint4 a = make_uint4(dv[0], (uint32_t)cv[0], dv[1], (uint32_t)cv[1]);
+    const uint4 b = make_uint4(dv[2], (uint32_t)cv[2], dv[3], (uint32_t)cv[3]);
+    __builtin_nontemporal_store(__builtin_bit_cast(v4nt, a), reinterpret_cast<v4nt*>(o));
+    __builtin_nontemporal_store(__builtin_bit_cast(v4nt, b), reinterpret_cast<v4nt*>(o) + 1);
+}
+
 // ------------------------------------------------------------------ class planes
 // grid: x -> 4 consecutive plane columns u per thread, y -> plane row v, z -> pair * nclass +
 // class.  Element (u, v) is the window value at level core position (x, y) = (u - 40, v - 40)
@@ -198,8 +211,7 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
     }
     // (D, C) pairs, row-major: one 8-B element per plane column
     uint4* o = reinterpret_cast<uint4*>(base) + ((long long)v * C.PW + 4 * j) / 2;
-    o[0] = make_uint4(dv[0], (uint32_t)cv[0], dv[1], (uint32_t)cv[1]);
-    o[1] = make_uint4(dv[2], (uint32_t)cv[2], dv[3], (uint32_t)cv[3]);
+    cls_store(o, dv, cv);
 }
 
 // Levels with at most 4 residue classes (the finest ones, whose Scharr planes are the largest):
@@ -286,8 +298,7 @@ __global__ __launch_bounds__(256) void k_lk_class_fused(const uint8_t* __restric
         }
         uint8_t* base = cls_out + (long long)pair * a.plan.bytes_per_pair + C.off + (long long)cls * C.class_bytes;
         uint4* o = reinterpret_cast<uint4*>(base) + ((long long)v * C.PW + 4 * j) / 2;
-        o[0] = make_uint4(dv[0], (uint32_t)cv[0], dv[1], (uint32_t)cv[1]);
-        o[1] = make_uint4(dv[2], (uint32_t)cv[2], dv[3], (uint32_t)cv[3]);
+        cls_store(o, dv, cv);
     }
 }
 
