@@ -109,8 +109,9 @@ def make_batch(w: int, h: int, batch: int, unique: int, seed0: int, threads: int
 
 
 def host_cores() -> dict:
-    """What this host offers: nproc (the CPUs this process may run on) and the cgroup CPU quota,
-    which on a shared GPU box can be far smaller than nproc."""
+    """What this host offers: nproc (the CPUs this process may run on), the cgroup CPU quota, which
+    on a shared GPU box can be far smaller than nproc (256 CPUs visible, 16 granted), and the CPUs
+    actually available = min(nproc, quota): the thread count the CPU baseline uses and reports."""
     nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     quota = None
     try:
@@ -119,7 +120,21 @@ def host_cores() -> dict:
             quota = round(int(q) / int(per), 2)
     except (OSError, ValueError):
         pass
-    return {"nproc": nproc, "cgroup_cpu_quota": quota}
+    avail = nproc if quota is None else max(1, min(nproc, int(quota)))
+    return {"nproc": nproc, "cgroup_cpu_quota": quota, "available": avail}
+
+
+def stamped_pmc(path: str, key: str, expect: str):
+    """A counter summary under profiles/ only when it was measured on the sources of the loaded
+    library: its src_sha256 (the bench line's build stamp in the profiled run) must equal this
+    build's, and its config string must match.  Otherwise None (the line then carries null)."""
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pj = json.load(f)
+    if pj.get("config") != expect or pj.get("src_sha256") != mdx._lib.build_info().get("src_sha256"):
+        return None
+    return pj
 
 
 def cpu_baseline(uniq, w, h, seconds: float, threads: int):
@@ -234,8 +249,25 @@ def spawn_ranks(n: int) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    return max(rcs, key=abs) if any(rcs) else 0
+    # poll every child: as soon as one rank fails, end its siblings (they would otherwise sit in a
+    # gloo collective waiting for it) and return that rank's code
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return bad[0]
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(0.2)
 
 
 def probe_ranks(D: Dist) -> None:
@@ -559,12 +591,8 @@ def main():
         launch_ms = rs["warp_diff"] / max(rs["calls"], 1)
         alg_bytes = 3.0 * RB * rw * rh     # read gray1 + read gray2 + write mask, 1 B/px each
         achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(args.pmc_json):
-            with open(args.pmc_json) as f:
-                pmc = json.load(f)
-            if pmc.get("config") == f"{rw}x{rh}x{RB}":
-                traffic = pmc.get("hbm_bytes_per_launch")
+        pmc = stamped_pmc(args.pmc_json, "config", f"{rw}x{rh}x{RB}")
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, kernel="k_warp_diff",
                     workload=f"{rw}x{rh} gray, {RB} pairs per launch, true H (affine), 3 B/px algorithmic",
@@ -578,8 +606,8 @@ def main():
     cpu = cpu1 = None
     if D.world == 1 and not args.no_cpu:
         hc = host_cores()
-        cpu = cpu_baseline(uniq, w, h, args.cpu_seconds, hc["nproc"])   # all host cores (nproc), stated
-        cpu.update(hc)
+        cpu = cpu_baseline(uniq, w, h, args.cpu_seconds, hc["available"])   # every CPU this job may use
+        cpu.update(nproc=hc["nproc"], cgroup_cpu_quota=hc["cgroup_cpu_quota"])
         cpu1 = cpu_baseline(uniq, w, h, args.cpu_seconds, 1)             # one core
     live = None
     if D.world == 1 and not args.no_live and not args.only_roofline:
@@ -599,13 +627,9 @@ def main():
                            iteration=LK_VALU_PER_ELEM_ITER, gradient_sums=LK_VALU_PER_ELEM_A),
                        workload=f"{B} pairs {w}x{h}, pixel_step {ps}, {wk['levels']} levels", **{
                            k: v for k, v in wk.items() if k not in ("valu_lane_instr_per_pair", "levels")})
-        pmc = os.path.join(ROOT, "profiles", "pmc_lk_iter.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                pj = json.load(f)
-            if pj.get("config") == f"{w}x{h}x{B}_ps{ps}":
-                lk_roof["executed_wave_instr_per_step"] = pj.get("sq_insts_valu_per_step")
-                lk_roof["executed_over_algorithmic"] = round(pj["sq_insts_valu_per_step"] / alg_wave, 3)
+        pj = stamped_pmc(os.path.join(ROOT, "profiles", "pmc_lk_iter.json"), "config", f"{w}x{h}x{B}_ps{ps}")
+        lk_roof["executed_wave_instr_per_step"] = pj.get("sq_insts_valu_per_step") if pj else None
+        lk_roof["executed_over_algorithmic"] = round(pj["sq_insts_valu_per_step"] / alg_wave, 3) if pj else None
     out = {
         "metric": METRIC,
         "value": round(value, 2),

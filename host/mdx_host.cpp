@@ -123,8 +123,8 @@ void MotionDetectionNode::run_pair(const Image& a, const Image& b, FrameResult* 
         const int x = (k / ny) * ps, y = (k % ny) * ps;          // x-major grid (:56-64)
         std::memcpy(&r->vector_image[((size_t)y * w + x) * 4], &vec[(size_t)4 * k], 32);
     }
-    publish("optical_flow_image", flow_image(a, r->vector_image, ps, p_.min_vector_size));   // :83-85
-    publish("motion_mask_image", mask_image(r->mask, w, h));
+    publish(kTopicFlowMarkers, flow_image(a, r->vector_image, ps, p_.min_vector_size));   // (not :83-85's arrows)
+    publish(kTopicMask, mask_image(r->mask, w, h));
 }
 
 // runOpticalFlowTrajectory (node.cpp:94-110) and, with egomotion, fitSubspace (:341-348)
@@ -156,7 +156,7 @@ void MotionDetectionNode::run_live(const std::vector<Image>& imgs, FrameResult* 
     r->trajectories.clear();
     for (int k = 0; k < npts; k++)                              // full-length ones only (:244-249)
         if (tlen[k] == nimg) r->trajectories.emplace_back(&traj[(size_t)k * nimg * 2], &traj[(size_t)(k + 1) * nimg * 2]);
-    publish("optical_flow_image", flow_image(imgs.back(), r->vector_image, ps, p_.min_vector_size));   // :101-103
+    publish(kTopicFlowMarkers, flow_image(imgs.back(), r->vector_image, ps, p_.min_vector_size));   // (not :101-103's arrows)
     r->outlier_points.clear();
     r->subspace_columns.clear();
     if (r->trajectories.empty() || !p_.egomotion) return;       // :296-318 / :357-389 (clustering: out of scope)

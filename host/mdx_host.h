@@ -104,10 +104,14 @@ private:
     long global_frame_count_ = 0;
 };
 
-// RGB8 renderings the node publishes: the motion mask replicated to three channels (the new,
-// optional ~motion_mask_image topic of SURVEY.md §8b), and the frame with a CV_RGB(0, 0, 255)
-// mark at each drawn vector's start point -- a point-marker stand-in for
-// showOpticalFlowVectors' anti-aliased arrows (optical_flow_visualizer.cpp:23-71, out of scope).
+// RGB8 renderings the node publishes, both under topic names of this build's own (kTopicMask,
+// kTopicFlowMarkers), never under the reference's: the motion mask replicated to three channels
+// (the new, optional mask topic of SURVEY.md §8b), and the frame with a CV_RGB(0, 0, 255) mark at
+// each vector showOpticalFlowVectors would draw.  The reference's ~optical_flow_image carries
+// anti-aliased arrows (optical_flow_visualizer.cpp:23-71, published at node.cpp:83-85, :101-103);
+// its rendering is out of scope, so that topic is not published here ("Topics").
+constexpr const char* kTopicMask = "motion_mask_image";
+constexpr const char* kTopicFlowMarkers = "mdx_flow_markers_image";
 Image mask_image(const std::vector<uint8_t>& mask, int w, int h);
 Image flow_image(const Image& rgb, const std::vector<double>& vector_image, int pixel_step, double min_vector_size);
 

@@ -15,7 +15,8 @@
 //                                 i32 ncols, i32 columns[ncols]
 //   flow_<k>_h, flow_<k>_f        writeFlow of the node's vector image (optical_flow_calculator.cpp:509)
 //   traj_<k>                      writeTrajectories (live path, :543)
-//   motion.log                    MotionLogger bounding box of the mask's moving pixels per frame
+// (The reference's MotionLogger logs the live branch's cluster rectangles, node.cpp:431-434; the
+// clustering is out of scope, so no motion.log is written.)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -98,7 +99,6 @@ int main(int argc, char** argv)
             write_bytes(out + "/pub_" + std::to_string(k) + "_" + topic + ".rgb8", im.data.data(), im.data.size());
         };
         MotionDetectionNode node(p, device, (int)frames[0].width, (int)frames[0].height, pub);
-        MotionLogger log(out + "/motion.log");
         for (size_t fi = 0; fi < frames.size(); fi++) {
             FrameResult r;
             if (!node.image_callback(frames[fi], &r)) continue;
@@ -112,17 +112,6 @@ int main(int argc, char** argv)
                 put(r.next_pts.data(), r.next_pts.size() * 4);
                 put(r.status.data(), r.status.size());
                 put(r.mask.data(), r.mask.size());
-                // MotionLogger: the bounding box of the moving pixels (frame, id 0), when any
-                int x0 = r.w, y0 = r.h, x1 = -1, y1 = -1;
-                for (int y = 0; y < r.h; y++)
-                    for (int x = 0; x < r.w; x++)
-                        if (r.mask[(size_t)y * r.w + x]) {
-                            x0 = std::min(x0, x);
-                            y0 = std::min(y0, y);
-                            x1 = std::max(x1, x);
-                            y1 = std::max(y1, y);
-                        }
-                if (x1 >= 0) log.write_bounding_box(x0, y0, x1 - x0 + 1, y1 - y0 + 1, (int)node.global_frame_count() - 1, 0);
             } else {
                 for (const auto& t : r.trajectories) put(t.data(), t.size() * 4);
                 put(r.outlier_points.data(), r.outlier_points.size() * 4);

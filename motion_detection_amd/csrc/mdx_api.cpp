@@ -42,6 +42,7 @@ struct mdx_ctx {
     bool lk_debug = false;
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
+    int lk_sub = 0;                          // > 0: LK sub-batch cap (MDX_LK_SUB, tests)
     int plan_w = -1, plan_h = -1, plan_ps = -1, plan_ml = -1, plan_gy0 = -1, plan_gy1 = -1;
     int band_w = 0, band_h = 0;              // frame of the last mdx_band_flow_dev (its pyramids are live)
     ClassPlan plan{};
@@ -314,6 +315,7 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     c->max_batch = max_batch;
     if (const char* e = std::getenv("MDX_LK_IMPL")) c->lk_impl = std::atoi(e) == 1 ? 1 : 2;
     if (const char* e = std::getenv("MDX_LK_G")) c->lk_g = std::atoi(e);
+    if (const char* e = std::getenv("MDX_LK_SUB")) c->lk_sub = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         g_create_err = "hipStreamCreate failed";
@@ -473,6 +475,7 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
         return MDX_OK;
     }
     a.plan = c->plan;
+    a.max_sub = c->lk_sub;
     a.cmap = c->ctab.as<int16_t>();
     a.rlist = c->ctab.as<int16_t>() + kMaxLevels * 2 * 128;
     a.ord = c->ctab.as<int16_t>() + 2 * kMaxLevels * 2 * 128;

@@ -102,6 +102,7 @@ struct LkArgs {
     const int16_t* ord;      // per level: nxp padded grid columns (-1 = empty), then ny grid rows,
                              // both grouped by residue class (ClassLevel::ord_off)
     const float* prev_pts;   // k_lk only: [batch][npts][2] start points (trajectories); null = the grid
+    int max_sub;             // > 0: at most this many pairs per LK sub-batch (MDX_LK_SUB, tests)
     float4* dbg;             // optional [batch][nlev][npts] (npx, npy, iters, status) at level end
     int dbg_pt;              // point whose per-iteration values are appended after dbg (pair 0)
 };

@@ -1142,12 +1142,14 @@ static hipError_t launch_front_bands(hipStream_t s, FrontArgs& a, int mode)
     auto lds_of = [&](int rb) { return (size_t)(2 * rb + 3) * a.lp + (size_t)rb * a.lp1; };
     const int rb = lds_of(4) <= 32 * 1024 ? 4 : lds_of(2) <= 64 * 1024 ? 2 : 1;
     const size_t lds = lds_of(rb);
-    if (lds > 160 * 1024) return hipErrorInvalidValue;   // rows wider than ~31K px
+    // k_front's static arrays (out0, out1, nout) share the CU's 160 KB with the dynamic rows
+    const size_t lds_static = (size_t)(2 * rb + 80 + rb + 80 + 2) * sizeof(int);
+    if (lds + lds_static > 160 * 1024) return hipErrorInvalidValue;   // rows wider than ~31K px
     a.nbands = (a.L1.h + rb - 1) / rb;
     const dim3 grid((unsigned)(a.nbands * a.nz));
 #define MDX_FRONT_CASE(M, R)                                                                             \
     if (mode == M && rb == R) {                                                                          \
-        if (lds > 64 * 1024)                                                                             \
+        if (lds + lds_static > 64 * 1024)                                                                \
             if (hipError_t e = hipFuncSetAttribute((const void*)k_front<R, M>,                           \
                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) \
                 return e;                                                                                \

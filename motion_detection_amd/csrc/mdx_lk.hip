@@ -850,7 +850,7 @@ static void launch_A(hipStream_t s, int batch, const LkArgs& a, const uint8_t* c
     constexpr int S = LkShape<G, UW>::S;
     const int ngroups = lk_groups<G, UW>(a, l);
     const dim3 grid((ngroups + S - 1) / S, batch);
-    if (l == a.maxl && !std::getenv("MDX_LK_A_DMA_ALL"))   // env: A/B of the two forms (timing only)
+    if (l == a.maxl)   // the coarsest level runs before any iteration launch (see k_lk_A_rows)
         hipLaunchKernelGGL((k_lk_A_rows<G, UW>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups);
     else
         hipLaunchKernelGGL((k_lk_A<G, UW>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups);
@@ -877,7 +877,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
     const long long span = std::max(a.plan.bytes_per_pair, a.g.img_bytes);
     int sub = batch;
     while (sub > 1 && ((sub + 7) / 8 + 1) * span > 0x7fff0000LL) sub = std::max(1, sub / 2);
-    if (const char* e = std::getenv("MDX_LK_SUB")) sub = std::max(1, std::min(sub, std::atoi(e)));   // tests
+    if (a.max_sub > 0) sub = std::max(1, std::min(sub, a.max_sub));   // MDX_LK_SUB (tests), read at mdx_create
     // Class planes and A sums depend on the previous frame only, not on the flow: with an aux
     // stream they run ahead (level L-1's while level L iterates, filling that kernel's tail);
     // every level has its own class planes, A buffer and queue heads, so nothing is overwritten

@@ -16,12 +16,13 @@ encoding, step, data).  Parameters mirror the node's ROS params (:29-44, :237-24
 Publishing is a callback: ``on_result(result)`` receives the FlowResult (vectors + mask),
 standing in for publishImage on ~optical_flow_image (:83-85).
 
-With ``live_chain=True`` the callback follows the reference's live branch instead (:266-348):
-every ring frame goes to calculateOpticalFlowTrajectory (:295, runOpticalFlowTrajectory
-:94-110); with egomotion and at least one complete trajectory, fitSubspace(trajectories,
-outlier_points, num_motions, sigma) follows (:341-348).  ``on_result`` then receives a LiveResult.
-The default (False) drives the pair path the north star names (runOpticalFlow, :76-92), the only
-one that produces the motion mask.
+By default (``live_chain=True``, as the reference's imageCallback and host/mdx_host.h) the callback
+follows the reference's live branch (:266-348): every ring frame goes to
+calculateOpticalFlowTrajectory (:295, runOpticalFlowTrajectory :94-110); with egomotion and at
+least one complete trajectory, fitSubspace(trajectories, outlier_points, num_motions, sigma) follows
+(:341-348).  ``on_result`` then receives a LiveResult.  ``live_chain=False`` drives the pair path
+the north star names (runOpticalFlow, :76-92) on the ring's last two frames, the only one that
+produces the motion mask.
 """
 from __future__ import annotations
 
@@ -79,10 +80,10 @@ class LiveResult:
 class MotionDetectionNode:
     def __init__(self, params: dict | None = None, on_result: Callable | None = None, device: int = 0):
         # the reference's defaults (node.cpp:29-44, :237-240, :346); egomotion true (:40) sets a
-        # ring of 2*num_motions+1 frames.  live_chain=False (the pair path) is this mirror's own
-        # default: the reference's imageCallback always runs the live branch.
+        # ring of 2*num_motions+1 frames, and imageCallback always runs the live branch on it
+        # (live_chain True; False selects the pair path on the ring's last two frames)
         self.params = {"pixel_step": 10, "min_vector_size": 1.0, "skip_frames": 1, "num_motions": 2,
-                       "egomotion": True, "use_all_frames": True, "sigma": 0.5, "live_chain": False}
+                       "egomotion": True, "use_all_frames": True, "sigma": 0.5, "live_chain": True}
         if params:
             self.params.update(params)
         self.on_result = on_result
@@ -115,7 +116,7 @@ class MotionDetectionNode:
             self.image_received = True
         out = None
         if self.params.get("use_all_frames", True) and self.image_received:
-            if self.params.get("live_chain", False):
+            if self.params.get("live_chain", True):
                 out = self.run_live_chain([to_rgb8(m) for m in self.raw_images])   # :266-295
             else:
                 frames = [to_rgb8(m) for m in list(self.raw_images)[-2:]]   # :266-287

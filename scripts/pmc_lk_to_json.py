@@ -3,8 +3,22 @@ Usage: python scripts/pmc_lk_to_json.py <dir> <steps covered by the run (warmup 
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
+
+
+def bench_stamp(d):
+    """src_sha256 of the library the profiled bench ran (its JSON line's build stamp, p1.json)."""
+    for f in sorted(glob.glob(os.path.join(d, "p*.json"))):
+        for line in open(f):
+            line = line.strip()
+            if line.startswith("{"):
+                try:
+                    return json.loads(line)["build"]["src_sha256"]
+                except (ValueError, KeyError, TypeError):
+                    pass
+    return None
 
 d, steps = sys.argv[1], int(sys.argv[2])
 tot = defaultdict(float)
@@ -25,5 +39,5 @@ out = {"kernels": "k_lk_class + k_lk_A + k_lk_iter", "config": f"{w}x{h}x{cfg['b
        "sq_insts_lds_per_step": tot["SQ_INSTS_LDS"] / steps,
        "per_kernel_valu_per_step": {k: v["SQ_INSTS_VALU"] / steps for k, v in per_kernel.items()},
        "counters_per_step": {k: v / steps for k, v in sorted(tot.items())},
-       "source": "scripts/pmc_lk.sh (rocprofv3 --pmc, two passes)"}
+       "source": "scripts/pmc_lk.sh (rocprofv3 --pmc, two passes)", "src_sha256": bench_stamp(d)}
 print(json.dumps(out, indent=1))

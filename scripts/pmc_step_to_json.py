@@ -15,6 +15,19 @@ import json
 import os
 import sys
 
+
+def bench_stamp(d):
+    """src_sha256 of the library the profiled bench ran (its JSON line's build stamp, p1.json)."""
+    for f in sorted(glob.glob(os.path.join(d, "p*.json"))):
+        for line in open(f):
+            line = line.strip()
+            if line.startswith("{"):
+                try:
+                    return json.loads(line)["build"]["src_sha256"]
+                except (ValueError, KeyError, TypeError):
+                    pass
+    return None
+
 d = sys.argv[1]
 out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_step.json")
 W, H, B = 1920, 1080, 32
@@ -39,6 +52,7 @@ for name, c in per.items():
 rows.sort(key=lambda x: -(x["read_mb"] + x["write_mb"]))
 px = W * H * B
 res = dict(workload=f"{W}x{H} gray, {B} pairs per step, pixel_step 10 (bench.py default step)", steps=steps,
+           config=f"{W}x{H}x{B}_ps10", src_sha256=bench_stamp(d),
            hbm_read_mb_per_step=round(tot_r / 1e6, 1), hbm_write_mb_per_step=round(tot_w / 1e6, 1),
            hbm_bytes_per_px=round((tot_r + tot_w) / px, 2), algorithmic_bytes_per_px=9.0,
            per_kernel=rows, correction="read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE",

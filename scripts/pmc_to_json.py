@@ -12,6 +12,19 @@ import json
 import os
 import sys
 
+
+def bench_stamp(d):
+    """src_sha256 of the library the profiled bench ran (its JSON line's build stamp, p1.json)."""
+    for f in sorted(glob.glob(os.path.join(d, "p*.json"))):
+        for line in open(f):
+            line = line.strip()
+            if line.startswith("{"):
+                try:
+                    return json.loads(line)["build"]["src_sha256"]
+                except (ValueError, KeyError, TypeError):
+                    pass
+    return None
+
 d, config = sys.argv[1], sys.argv[2]
 out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_warp_diff.json")
 w, h, b = (int(v) for v in config.split("x"))
@@ -33,6 +46,6 @@ res = dict(kernel="k_warp_diff", config=config, launches=len(vals["FETCH_SIZE"])
            read_bytes_per_launch=int(read_b), write_bytes_per_launch=int(write_b),
            hbm_bytes_per_launch=int(read_b + write_b), algorithmic_bytes_per_launch=3 * w * h * b,
            correction="read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE",
-           source=os.path.basename(os.path.normpath(d)))
+           source=os.path.basename(os.path.normpath(d)), src_sha256=bench_stamp(d))
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res))

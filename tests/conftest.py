@@ -20,12 +20,24 @@ def oracle():
     return pyoracle
 
 
+def _lib_stamp(path):
+    """The src_sha256 compiled into a libmdx.so (csrc/Makefile's mdx_build_info string), read from
+    the file's bytes without loading it."""
+    with open(path, "rb") as f:
+        data = f.read()
+    i = data.find(b"src_sha256=")
+    return data[i + 11:i + 75].decode() if i >= 0 else None
+
+
 @pytest.fixture(scope="session")
 def mdx():
+    """The in-tree libmdx.so, rebuilt from the tree (make -B) whenever it is missing or its stamp
+    does not match the sources here, so a test never runs a library built from other sources."""
     import motion_detection_amd as m
-    if not os.path.exists(m.LIB_PATH):
+    if not os.path.exists(m.LIB_PATH) or _lib_stamp(m.LIB_PATH) != m._lib.source_sha256():
         m.build()
     m.lib()
+    assert m._lib.build_info()["matches_tree"], "libmdx.so does not match the sources in the tree"
     return m
 
 

@@ -4,7 +4,7 @@ frame bytes and the C-ABI.
 Reference: MotionDetectionNode (ros/src/motion_detection_node.cpp) -- imageCallback's ring, skip
 and rgb8 semantics (:235-287), runOpticalFlow (:76-92), runOpticalFlowTrajectory + fitSubspace
 (:94-110, :341-348), publishImage's RGB8 messages (:217-223), writeFlow / writeTrajectories
-(common/src/optical_flow_calculator.cpp:509-562) and MotionLogger (common/src/motion_logger.cpp:31-47).
+(common/src/optical_flow_calculator.cpp:509-562) and MotionLogger's format (common/src/motion_logger.cpp:31-47).
 
 The tests write a recorded stream of sensor_msgs/Image-shaped frames to a file; the g++-built
 binary reads it, runs the node through libmdx.so and writes every published image and output.
@@ -170,8 +170,12 @@ def test_host_writers_match_python_formats(tmp_path, mdx):
 @pytest.mark.gpu
 @pytest.mark.parametrize("enc,skip", [("rgb8", 1), ("bgr8", 2), ("mono8", 1)])
 def test_node_pair_path_matches_oracle(node_exe, tmp_path, mdx, oracle, enc, skip):
-    """runOpticalFlow per processed frame: outputs, published RGB8 mask / flow images and the
-    writeFlow files equal the oracle's on the ring's last two rgb8 frames."""
+    """runOpticalFlow per processed frame, on the ring's last two rgb8 frames: the calculator's
+    outputs (next_pts, status, mask, H, num_vectors), the node's Vec4d vector image as writeFlow
+    writes it (optical_flow_calculator.cpp:509-541) and the comp mask on the build's own mask topic
+    equal the oracle's.  Only reference-defined bytes are pinned: no topic under a reference name
+    is published with content the reference does not define (~optical_flow_image's arrows are out
+    of scope), and no motion.log is written (the reference logs cluster rectangles, node.cpp:431)."""
     from motion_detection_amd.formats import write_flow
     w, h, ps, mvs = 320, 240, 10, 1.0
     seq = []
@@ -187,7 +191,6 @@ def test_node_pair_path_matches_oracle(node_exe, tmp_path, mdx, oracle, enc, ski
     kept = kept_frames(len(frames), skip)
     ring_pairs = [(kept[i - 1], kept[i]) for i in range(1, len(kept))]   # trajectory_size 2
     assert f"processed {len(ring_pairs)} of {len(frames)}" in p.stdout, p.stdout
-    log_lines = []
     for k, (i1, i2) in enumerate(ring_pairs):
         f1, f2 = to_rgb8(seq[i1], enc), to_rgb8(seq[i2], enc)
         ref = oracle.calculate_optical_flow(f1, f2, pixel_step=ps, min_vector_size=mvs)
@@ -199,25 +202,13 @@ def test_node_pair_path_matches_oracle(node_exe, tmp_path, mdx, oracle, enc, ski
         assert np.array_equal(r["H"], ref["H"])
         mask_pub = np.fromfile(out / f"pub_{k}_motion_mask_image.rgb8", np.uint8).reshape(h, w, 3)
         assert np.array_equal(mask_pub, np.repeat(ref["mask"][:, :, None], 3, axis=2))
+        assert not (out / f"pub_{k}_optical_flow_image.rgb8").exists()
         vi = vector_image(ref["vectors"], w, h, ps)
-        flow_pub = np.fromfile(out / f"pub_{k}_optical_flow_image.rgb8", np.uint8).reshape(h, w, 3)
-        exp = f1.copy()
-        d = vi[..., 2:]
-        sel = ((np.abs(d[..., 0]) > mvs) | (np.abs(d[..., 1]) > mvs)) & (np.abs(d[..., 0]) < 5 * ps) & \
-              (np.abs(d[..., 1]) < 5 * ps)
-        for y, x in zip(*np.nonzero(sel)):
-            sx, sy = int(vi[y, x, 0]), int(vi[y, x, 1])
-            if 0 <= sx < w and 0 <= sy < h:
-                exp[sy, sx] = (0, 0, 255)
-        assert np.array_equal(flow_pub, exp)
         pyf = str(tmp_path / f"py_flow_{k}")
         write_flow(vi, pyf, ps)
         for sfx in ("_h", "_f"):
             assert open(out / f"flow_{k}{sfx}", "rb").read() == open(pyf + sfx, "rb").read()
-        ys, xs = np.nonzero(ref["mask"])
-        if len(ys):   # MotionLogger::writeBoundingBox of the moving pixels' box (frame = counter at the call)
-            log_lines.append(f"{i2}, 0, {xs.min()}, {ys.min()}, {xs.max() + 1}, {ys.max() + 1}")
-    assert open(out / "motion.log").read().splitlines() == log_lines
+    assert not (out / "motion.log").exists()
 
 
 @pytest.mark.gpu

@@ -34,6 +34,7 @@ def frame(v, h=6, w=8, enc="mono8"):
 
 
 def make_node(**params):
+    params.setdefault("live_chain", False)   # these tests drive the pair path (runOpticalFlow)
     n = MotionDetectionNode(params)       # no device work at construction
     n.ofc = RecordingCalc()
     return n
@@ -68,9 +69,24 @@ def test_pairs_of_consecutive_frames():
 
 
 def test_reference_defaults():
-    n = make_node()
+    n = MotionDetectionNode()
     assert n.params["egomotion"] is True                     # node.cpp:40
+    assert n.params["live_chain"] is True                    # imageCallback's live branch (:266-348)
     assert n.trajectory_size == 5                            # 2*num_motions + 1 (:241)
+
+
+def test_default_first_result_is_the_live_branch_on_frame_4():
+    """Under the defaults the ring fills to 2*num_motions+1 = 5 frames and the fifth callback runs
+    the live branch on all five (node.cpp:241-295), as the reference and host/mdx_host.h do."""
+    n = MotionDetectionNode()
+    rec = RecordingLive()
+    n.ofc = rec
+    n.od = rec
+    out = [n.image_callback(frame(v)) for v in range(6)]
+    assert [i for i, o in enumerate(out) if o is not None] == [4, 5]
+    assert [im[0, 0, 0] for im in rec.traj_calls[0][0]] == [0, 1, 2, 3, 4]
+    assert [im[0, 0, 0] for im in rec.traj_calls[1][0]] == [1, 2, 3, 4, 5]
+    assert len(rec.fit_calls) == 2
 
 
 def test_egomotion_ring_size():
