@@ -82,6 +82,14 @@ bool MotionDetectionNode::image_callback(const Image& msg, FrameResult* out)
         raw_images_.pop_front();
         image_received_ = true;
     }
+    if (p_.live_path) {
+        // the device ring mirrors raw_images_: this frame is converted, uploaded and pyramided once
+        // (the reference re-converts every ring frame on every callback, :266-287)
+        last_rgb_ = to_rgb8(msg);
+        const int rc = mdx_ring_push(ctx_, last_rgb_.data.data(), (int)last_rgb_.width, (int)last_rgb_.height,
+                                     (int)last_rgb_.step, MDX_FMT_RGB8, (int)raw_images_.size());
+        if (rc < 0) throw std::runtime_error(std::string("mdx_ring_push: ") + mdx_last_error(ctx_));
+    }
     bool done = false;
     if (p_.use_all_frames && image_received_) {                  // :262
         mdx_params mp;
@@ -89,12 +97,14 @@ bool MotionDetectionNode::image_callback(const Image& msg, FrameResult* out)
         mp.pixel_step = p_.pixel_step;                           // re-read every frame (:264)
         mp.min_vector_size = p_.min_vector_size;
         if (mdx_set_params(ctx_, &mp) != MDX_OK) throw std::runtime_error(mdx_last_error(ctx_));
-        std::vector<Image> rgb;
-        for (const Image& m : raw_images_) rgb.push_back(to_rgb8(m));   // toCvCopy(*iter, "rgb8") :271
         FrameResult local;
         FrameResult* r = out ? out : &local;
-        if (p_.live_path) run_live(rgb, r);
-        else run_pair(rgb[rgb.size() - 2], rgb.back(), r);
+        if (p_.live_path) {
+            run_live((int)raw_images_.size(), r);
+        } else {
+            // toCvCopy(*iter, "rgb8") (:271) of the two frames the pair path reads
+            run_pair(to_rgb8(raw_images_[raw_images_.size() - 2]), to_rgb8(raw_images_.back()), r);
+        }
         done = true;
     }
     global_frame_count_++;
@@ -127,25 +137,22 @@ void MotionDetectionNode::run_pair(const Image& a, const Image& b, FrameResult* 
     publish(kTopicMask, mask_image(r->mask, w, h));
 }
 
-// runOpticalFlowTrajectory (node.cpp:94-110) and, with egomotion, fitSubspace (:341-348)
-void MotionDetectionNode::run_live(const std::vector<Image>& imgs, FrameResult* r)
+// runOpticalFlowTrajectory (node.cpp:94-110) over the nimg ring frames already on the device, and,
+// with egomotion, fitSubspace (:341-348)
+void MotionDetectionNode::run_live(int nimg, FrameResult* r)
 {
-    const int nimg = (int)imgs.size(), w = (int)imgs[0].width, h = (int)imgs[0].height, ps = p_.pixel_step;
+    const int w = (int)last_rgb_.width, h = (int)last_rgb_.height, ps = p_.pixel_step;
+    for (const Image& m : raw_images_)
+        if (m.width != last_rgb_.width || m.height != last_rgb_.height) throw std::invalid_argument("frame sizes differ");
     const int npts = mdx_grid_count(w, h, ps);
     r->w = w;
     r->h = h;
     r->npts = npts;
-    std::vector<const uint8_t*> ptrs;
-    for (const Image& im : imgs) {
-        if (im.width != imgs[0].width || im.height != imgs[0].height) throw std::invalid_argument("frame sizes differ");
-        ptrs.push_back(im.data.data());
-    }
     std::vector<float> traj((size_t)npts * nimg * 2), start((size_t)npts * 2);
     std::vector<int32_t> tlen(npts);
     std::vector<double> vec((size_t)npts * 4);
-    const int rc = mdx_flow_trajectory(ctx_, ptrs.data(), nimg, w, h, (int)imgs[0].step, MDX_FMT_RGB8, traj.data(),
-                                       tlen.data(), start.data(), vec.data(), &r->num_vectors);
-    if (rc < 0) throw std::runtime_error(std::string("mdx_flow_trajectory: ") + mdx_last_error(ctx_));
+    const int rc = mdx_ring_trajectory(ctx_, traj.data(), tlen.data(), start.data(), vec.data(), &r->num_vectors);
+    if (rc < 0) throw std::runtime_error(std::string("mdx_ring_trajectory: ") + mdx_last_error(ctx_));
     // optical_flow_vectors = zeros (:98); the last pass stores each point's Vec4d at
     // ((int)y, (int)x) of its position entering that pass, in point order
     r->vector_image.assign((size_t)w * h * 4, 0.0);
@@ -156,7 +163,7 @@ void MotionDetectionNode::run_live(const std::vector<Image>& imgs, FrameResult* 
     r->trajectories.clear();
     for (int k = 0; k < npts; k++)                              // full-length ones only (:244-249)
         if (tlen[k] == nimg) r->trajectories.emplace_back(&traj[(size_t)k * nimg * 2], &traj[(size_t)(k + 1) * nimg * 2]);
-    publish(kTopicFlowMarkers, flow_image(imgs.back(), r->vector_image, ps, p_.min_vector_size));   // (not :101-103's arrows)
+    publish(kTopicFlowMarkers, flow_image(last_rgb_, r->vector_image, ps, p_.min_vector_size));   // (not :101-103's arrows)
     r->outlier_points.clear();
     r->subspace_columns.clear();
     if (r->trajectories.empty() || !p_.egomotion) return;       // :296-318 / :357-389 (clustering: out of scope)

@@ -92,7 +92,7 @@ public:
 
 private:
     void run_pair(const Image& a, const Image& b, FrameResult* r);
-    void run_live(const std::vector<Image>& imgs, FrameResult* r);
+    void run_live(int nimg, FrameResult* r);
     void publish(const std::string& topic, const Image& img) const;
 
     Params p_;
@@ -100,6 +100,7 @@ private:
     mdx_ctx* ctx_ = nullptr;
     mdx_rand_state rng_{};
     std::deque<Image> raw_images_;
+    Image last_rgb_;                          // the newest frame as rgb8 (also in the device ring)
     bool image_received_ = false;
     long global_frame_count_ = 0;
 };

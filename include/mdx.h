@@ -203,6 +203,25 @@ int mdx_flow_trajectory(mdx_ctx* ctx, const uint8_t* const* imgs, int nimg, int 
                         int* num_vectors);
 
 /*
+ * Resident frame ring for the live chain: the node's raw_images_ deque (motion_detection_node.h:82,
+ * filled at node.cpp:248-261), whose every frame the reference re-converts, re-uploads and
+ * re-pyramids on each callback (:266-287, then optical_flow_calculator.cpp:166-170).  Here a frame
+ * crosses PCIe and is pyramided (gray, padded levels, Scharr planes) once, when it enters the ring,
+ * and stays in HBM while it is in it.
+ *   mdx_ring_push        append a frame (w x h, row pitch `stride`, format `fmt`), then drop frames
+ *                        from the front until at most `keep` remain (the deque's size after the
+ *                        reference's push / pop at :248-261).  A frame of another size empties the
+ *                        ring first.  Returns the number of frames held, or a negative error.
+ *   mdx_ring_trajectory  calculateOpticalFlowTrajectory over the frames held (>= 2), outputs exactly
+ *                        as mdx_flow_trajectory's (nimg = the ring size).
+ *   mdx_ring_reset       empty the ring.
+ */
+int mdx_ring_push(mdx_ctx* ctx, const uint8_t* img, int w, int h, int stride, int fmt, int keep);
+int mdx_ring_trajectory(mdx_ctx* ctx, float* traj, int32_t* traj_len, float* start_pts, double* vectors,
+                        int* num_vectors);
+int mdx_ring_reset(mdx_ctx* ctx);
+
+/*
  * Trajectory subspace RANSAC: replaces OutlierDetector::fitSubspace
  * (common/include/motion_detection/outlier_detector.h:21, outlier_detector.cpp:236-331), called
  * by the node on the complete trajectories (motion_detection_node.cpp:348).

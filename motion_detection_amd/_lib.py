@@ -36,10 +36,11 @@ EXPORTED = [
     "mdx_dev_free", "mdx_memcpy_h2d", "mdx_memcpy_d2h", "mdx_enable_timing", "mdx_timing_calls", "mdx_stage_ms",
     "mdx_synth_pair", "mdx_debug_copy", "mdx_band_flow_dev", "mdx_band_fit_warp_dev", "mdx_flow_trajectory",
     "mdx_srand", "mdx_rand", "mdx_fit_subspace", "mdx_device_pci", "mdx_build_info",
+    "mdx_ring_push", "mdx_ring_trajectory", "mdx_ring_reset",
 ]
 
 # csrc/Makefile STAMPED: the files whose bytes the library's provenance stamp hashes, in order
-STAMPED = ["Makefile", "mdx_internal.h", "mdx_api.cpp", "mdx_kernels.hip", "mdx_lk.hip", "mdx_warp.hip",
+STAMPED = ["Makefile", "mdx_internal.h", "mdx_api.cpp", "mdx_kernels.hip", "mdx_lk.hip", "mdx_lkpt.hip", "mdx_warp.hip",
            "mdx_subspace.hip", "synth.cpp", os.path.join("..", "..", "include", "mdx.h")]
 
 
@@ -167,6 +168,12 @@ def lib() -> C.CDLL:
     L.mdx_flow_trajectory.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp,
                                       C.POINTER(C.c_int)]
     L.mdx_flow_trajectory.restype = C.c_int
+    L.mdx_ring_push.argtypes = [vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+    L.mdx_ring_push.restype = C.c_int
+    L.mdx_ring_trajectory.argtypes = [vp, vp, vp, vp, vp, C.POINTER(C.c_int)]
+    L.mdx_ring_trajectory.restype = C.c_int
+    L.mdx_ring_reset.argtypes = [vp]
+    L.mdx_ring_reset.restype = C.c_int
     L.mdx_srand.argtypes = [C.POINTER(MdxRandState), C.c_uint32]
     L.mdx_srand.restype = None
     L.mdx_rand.argtypes = [C.POINTER(MdxRandState)]

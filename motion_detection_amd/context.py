@@ -165,6 +165,30 @@ class Context:
                                               _ptr(tlen), _ptr(start), _ptr(vec), C.byref(num)))
         return TrajectoryResult(num.value, traj, tlen, start, vec)
 
+    # -- resident frame ring (the node's raw_images_ deque kept in HBM: mdx_ring_*)
+    def ring_push(self, image: np.ndarray, keep: int, fmt: int | None = None) -> int:
+        """Append one frame (pyramided once, on the device) and keep at most `keep` frames.
+        Returns the number of frames held."""
+        im = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = im.shape[:2]
+        if fmt is None:
+            fmt = _lib.FMT_GRAY8 if im.ndim == 2 else _lib.FMT_RGB8
+        return self._check(lib().mdx_ring_push(self._h, _ptr(im), w, h, im.strides[0], fmt, int(keep)))
+
+    def ring_trajectory(self, w: int, h: int, nimg: int) -> "TrajectoryResult":
+        """calculateOpticalFlowTrajectory over the ring's `nimg` frames (w x h)."""
+        n = grid_count(w, h, self.params.pixel_step)
+        traj = np.zeros((n, nimg, 2), np.float32)
+        tlen = np.zeros(n, np.int32)
+        start = np.zeros((n, 2), np.float32)
+        vec = np.zeros((n, 4), np.float64)
+        num = C.c_int(0)
+        self._check(lib().mdx_ring_trajectory(self._h, _ptr(traj), _ptr(tlen), _ptr(start), _ptr(vec), C.byref(num)))
+        return TrajectoryResult(num.value, traj, tlen, start, vec)
+
+    def ring_reset(self) -> None:
+        self._check(lib().mdx_ring_reset(self._h))
+
     # -- trajectory subspace RANSAC (drop-in for OutlierDetector::fitSubspace)
     def fit_subspace(self, traj: np.ndarray, num_motions: int, sigma: float, rng: "_lib.MdxRandState") -> "SubspaceResult":
         traj = np.ascontiguousarray(traj, dtype=np.float32)

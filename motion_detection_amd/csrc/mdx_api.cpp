@@ -39,8 +39,12 @@ struct mdx_ctx {
     DevBuf csum;                             // classify: per-block summaries
     DevBuf tin, tcur, tnp, tst, ttraj, tlen, tvec, tstart, tnum;   // trajectory tracking
     DevBuf straj, sdata, sq, scnt, scols, sres, sout, sbest;      // subspace RANSAC
+    DevBuf ring_pyr, ring_der, rin;          // resident frame ring (mdx_ring_*)
+    std::vector<int> ring_order;             // held slots, oldest first
+    int ring_cap = 0, ring_w = 0, ring_h = 0, ring_ml = -1;
     bool lk_debug = false;
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
+    bool lk_pts = false;                     // arbitrary start points: k_lk (MDX_LK_PTS=1: k_lk_pts)
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
     int lk_sub = 0;                          // > 0: LK sub-batch cap (MDX_LK_SUB, tests)
     int plan_w = -1, plan_h = -1, plan_ps = -1, plan_ml = -1, plan_gy0 = -1, plan_gy1 = -1;
@@ -316,6 +320,7 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     if (const char* e = std::getenv("MDX_LK_IMPL")) c->lk_impl = std::atoi(e) == 1 ? 1 : 2;
     if (const char* e = std::getenv("MDX_LK_G")) c->lk_g = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_SUB")) c->lk_sub = std::atoi(e);
+    if (const char* e = std::getenv("MDX_LK_PTS")) c->lk_pts = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         g_create_err = "hipStreamCreate failed";
@@ -351,7 +356,7 @@ extern "C" int mdx_destroy(mdx_ctx* c)
                       &c->vec, &c->mask, &c->H, &c->Hext, &c->num, &c->bnp, &c->bst,
                       &c->cls, &c->Abuf, &c->ctab, &c->dbg, &c->csum, &c->tin, &c->tcur, &c->tnp, &c->tst,
                       &c->ttraj, &c->tlen, &c->tvec, &c->tstart, &c->tnum, &c->straj, &c->sdata, &c->sq,
-                      &c->scnt, &c->scols, &c->sres, &c->sout, &c->sbest};
+                      &c->scnt, &c->scols, &c->sres, &c->sout, &c->sbest, &c->ring_pyr, &c->ring_der, &c->rin};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (c->ev) {
@@ -471,7 +476,7 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
         if (!have_scharr)
             for (int l = 0; l < g.nlev; l++)
                 HIP_OR_RETURN(c, launch_scharr(s, batch, a.pyr1, const_cast<uint32_t*>(a.der), g, l));
-        HIP_OR_RETURN(c, launch_lk(s, batch, a));
+        HIP_OR_RETURN(c, c->lk_pts ? launch_lk_pts(s, batch, a) : launch_lk(s, batch, a));
         return MDX_OK;
     }
     a.plan = c->plan;
@@ -659,33 +664,20 @@ extern "C" int mdx_flow_warp_diff(mdx_ctx* c, const uint8_t* img1, const uint8_t
     return MDX_OK;
 }
 
-// calculateOpticalFlowTrajectory (optical_flow_calculator.cpp:133-257).  Pair slot j holds
-// frames (j, j+1): the gray / pyramid / Scharr stages run batched over all slots in one launch
-// each (the reference rebuilds each frame's pyramid twice, :166-170; these are the same images),
-// then the nimg-1 LK passes run in order on the points the previous pass left.
-extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int nimg, int w, int h, int stride,
-                                   int fmt, float* traj, int32_t* traj_len, float* start_pts, double* vectors,
-                                   int* num_vectors)
+// The trajectory passes of calculateOpticalFlowTrajectory (optical_flow_calculator.cpp:143-257) over
+// nimg frames whose padded pyramids and Scharr planes are on the device already: pass j tracks the
+// points the previous pass left from frame j (pyr[j], der[j]) to frame j + 1 (pyr[j + 1]).  Every
+// pass runs the point LK from the carried points: for one pair it is faster than the class-plane
+// kernels even on the grid start points of pass 0, whose per-level tails one pair cannot fill.
+static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int h, const uint8_t* const* pyr,
+                             const uint32_t* const* der, float* traj, int32_t* traj_len, float* start_pts,
+                             double* vectors, int* num_vectors)
 {
-    if (!c) return MDX_EINVAL;
-    if (!imgs || nimg < 2) return set_err(c, MDX_EINVAL, "mdx_flow_trajectory: need >= 2 frames");
-    for (int i = 0; i < nimg; i++)
-        if (!imgs[i]) return set_err(c, MDX_EINVAL, "mdx_flow_trajectory: null frame %d", i);
-    if (w <= 0 || h <= 0) return set_err(c, MDX_EINVAL, "bad frame size");
-    if (fmt < MDX_FMT_GRAY8 || fmt > MDX_FMT_BGR8) return set_err(c, MDX_EINVAL, "bad pixel format %d", fmt);
-    const int cn = fmt == MDX_FMT_GRAY8 ? 1 : 3;
-    if (stride < w * cn) return set_err(c, MDX_EINVAL, "stride %d < w*channels %d", stride, w * cn);
-    HIP_OR_RETURN(c, hipSetDevice(c->device));
     const mdx_params& P = c->prm;
-    const int npairs = nimg - 1;
-    const Geometry g = make_geometry(w, h, P.max_level);
-    int rc = ensure_workspace(c, g, npairs);
-    if (rc != MDX_OK) return rc;
     const int npts = mdx_grid_count(w, h, P.pixel_step);
     const int ny = (h + P.pixel_step - 1) / P.pixel_step;
     const size_t pts = (size_t)(npts > 0 ? npts : 1);
-    const size_t fbytes = (size_t)stride * h;
-    if ((rc = ensure(c, c->tin, fbytes * nimg)) != MDX_OK) return rc;
+    int rc;
     if ((rc = ensure(c, c->tcur, pts * 8)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->tnp, pts * 8)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->tst, pts)) != MDX_OK) return rc;
@@ -694,27 +686,17 @@ extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int n
     if ((rc = ensure(c, c->tvec, pts * 32)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->tstart, pts * 8)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->tnum, 4)) != MDX_OK) return rc;
-
     hipStream_t s = c->stream;
-    uint8_t* din = c->tin.as<uint8_t>();
-    for (int i = 0; i < nimg; i++)
-        HIP_OR_RETURN(c, hipMemcpyAsync(din + fbytes * i, imgs[i], fbytes, hipMemcpyHostToDevice, s));
-    uint8_t* pyr1 = c->pyr1.as<uint8_t>();
-    uint8_t* pyr2 = c->pyr2.as<uint8_t>();
-    uint32_t* der = c->der.as<uint32_t>();
-    HIP_OR_RETURN(c, launch_front(s, npairs, din, din + fbytes, w, h, stride, (long long)fbytes, fmt, pyr1, pyr2, g));
-    HIP_OR_RETURN(c, launch_pyr_levels(s, npairs, pyr1, pyr2, g));
-    for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, npairs, pyr1, der, g, l));
     float* cur = c->tcur.as<float>();
     float* tr = c->ttraj.as<float>();
     int* tl = c->tlen.as<int>();
     int* dnum = c->tnum.as<int>();
     HIP_OR_RETURN(c, launch_traj_init(s, npts, ny, P.pixel_step, nimg, cur, tr, tl, dnum));
-    for (int j = 0; j < npairs && npts > 0; j++) {
+    for (int j = 0; j + 1 < nimg && npts > 0; j++) {
         LkArgs a{};
-        a.pyr1 = pyr1 + (size_t)g.img_bytes * j;
-        a.pyr2 = pyr2 + (size_t)g.img_bytes * j;
-        a.der = der + (size_t)g.der_words * j;
+        a.pyr1 = pyr[j];
+        a.pyr2 = pyr[j + 1];
+        a.der = der[j];
         a.g = g;
         a.maxl = g.nlev - 1;
         a.npts = npts;
@@ -727,13 +709,10 @@ extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int n
         a.eps2 = e * e;
         a.next_pts = c->tnp.as<float>();
         a.status = c->tst.as<uint8_t>();
-        // every pass on the single-kernel LK from the carried points: for one pair it is faster
-        // than the class-plane kernels even on the grid start points of pass 0 (live leg 4.7 vs
-        // 5.2 ms), whose per-level tails one pair cannot fill
         a.prev_pts = cur;
         if ((rc = run_lk(c, g, a, 1, w, h, 0, ny, true)) != MDX_OK) return rc;
         HIP_OR_RETURN(c, launch_traj_update(s, npts, c->tnp.as<float>(), c->tst.as<uint8_t>(), cur, tr, tl, nimg, w, h,
-                                            j == npairs - 1, P.min_vector_size, c->tvec.as<double>(),
+                                            j == nimg - 2, P.min_vector_size, c->tvec.as<double>(),
                                             c->tstart.as<float>(), dnum));
     }
     int num = 0;
@@ -747,6 +726,161 @@ extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int n
     HIP_OR_RETURN(c, hipStreamSynchronize(s));
     if (num_vectors) *num_vectors = num;
     return MDX_OK;
+}
+
+static int check_frame(mdx_ctx* c, const char* who, int w, int h, int stride, int fmt)
+{
+    if (w <= 0 || h <= 0) return set_err(c, MDX_EINVAL, "%s: bad frame size", who);
+    if (fmt < MDX_FMT_GRAY8 || fmt > MDX_FMT_BGR8) return set_err(c, MDX_EINVAL, "%s: bad pixel format %d", who, fmt);
+    const int cn = fmt == MDX_FMT_GRAY8 ? 1 : 3;
+    if (stride < w * cn) return set_err(c, MDX_EINVAL, "%s: stride %d < w*channels %d", who, stride, w * cn);
+    return MDX_OK;
+}
+
+// calculateOpticalFlowTrajectory (optical_flow_calculator.cpp:133-257) on host frames.  Pair slot j
+// holds frames (j, j+1): the gray / pyramid / Scharr stages run batched over all slots in one
+// launch each (the reference rebuilds each frame's pyramid twice, :166-170; these are the same
+// images), then the nimg-1 LK passes run in order on the points the previous pass left.
+extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int nimg, int w, int h, int stride,
+                                   int fmt, float* traj, int32_t* traj_len, float* start_pts, double* vectors,
+                                   int* num_vectors)
+{
+    if (!c) return MDX_EINVAL;
+    if (!imgs || nimg < 2) return set_err(c, MDX_EINVAL, "mdx_flow_trajectory: need >= 2 frames");
+    for (int i = 0; i < nimg; i++)
+        if (!imgs[i]) return set_err(c, MDX_EINVAL, "mdx_flow_trajectory: null frame %d", i);
+    int rc = check_frame(c, "mdx_flow_trajectory", w, h, stride, fmt);
+    if (rc != MDX_OK) return rc;
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    const int npairs = nimg - 1;
+    const Geometry g = make_geometry(w, h, c->prm.max_level);
+    if ((rc = ensure_workspace(c, g, npairs)) != MDX_OK) return rc;
+    const size_t fbytes = (size_t)stride * h;
+    if ((rc = ensure(c, c->tin, fbytes * nimg)) != MDX_OK) return rc;
+    hipStream_t s = c->stream;
+    uint8_t* din = c->tin.as<uint8_t>();
+    for (int i = 0; i < nimg; i++)
+        HIP_OR_RETURN(c, hipMemcpyAsync(din + fbytes * i, imgs[i], fbytes, hipMemcpyHostToDevice, s));
+    uint8_t* pyr1 = c->pyr1.as<uint8_t>();
+    uint8_t* pyr2 = c->pyr2.as<uint8_t>();
+    uint32_t* der = c->der.as<uint32_t>();
+    HIP_OR_RETURN(c, launch_front(s, npairs, din, din + fbytes, w, h, stride, (long long)fbytes, fmt, pyr1, pyr2, g));
+    HIP_OR_RETURN(c, launch_pyr_levels(s, npairs, pyr1, pyr2, g));
+    for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, npairs, pyr1, der, g, l));
+    // frame j's pyramid is slot j of pyr1 (j < nimg-1) and the last frame's slot nimg-2 of pyr2
+    std::vector<const uint8_t*> fp(nimg);
+    std::vector<const uint32_t*> fd(nimg);
+    for (int j = 0; j < npairs; j++) {
+        fp[j] = pyr1 + (size_t)g.img_bytes * j;
+        fd[j] = der + (size_t)g.der_words * j;
+    }
+    fp[npairs] = pyr2 + (size_t)g.img_bytes * (npairs - 1);
+    fd[npairs] = nullptr;
+    return trajectory_passes(c, g, nimg, w, h, fp.data(), fd.data(), traj, traj_len, start_pts, vectors, num_vectors);
+}
+
+// The resident ring (include/mdx.h): slot k of ring_pyr / ring_der holds one frame's padded pyramid
+// and Scharr planes; ring_order lists the held slots oldest first.
+static int ring_grow(mdx_ctx* c, const Geometry& g, int cap)
+{
+    if (cap <= c->ring_cap) return MDX_OK;
+    DevBuf np, nd;
+    auto fail = [&](const char* what) {
+        if (np.p) (void)hipFree(np.p);
+        if (nd.p) (void)hipFree(nd.p);
+        return set_err(c, MDX_ENOMEM, "mdx_ring_push: %s", what);
+    };
+    if (hipMalloc(&np.p, (size_t)g.img_bytes * cap) != hipSuccess) return fail("hipMalloc(pyramids)");
+    if (hipMalloc(&nd.p, (size_t)g.der_words * 4 * cap) != hipSuccess) return fail("hipMalloc(derivatives)");
+    np.cap = (size_t)g.img_bytes * cap;
+    nd.cap = (size_t)g.der_words * 4 * cap;
+    // the held frames move to slots 0 .. n-1, in order
+    for (size_t k = 0; k < c->ring_order.size(); k++) {
+        const int o = c->ring_order[k];
+        HIP_OR_RETURN(c, hipMemcpyAsync(np.as<uint8_t>() + (size_t)g.img_bytes * k, c->ring_pyr.as<uint8_t>() + (size_t)g.img_bytes * o,
+                                        g.img_bytes, hipMemcpyDeviceToDevice, c->stream));
+        HIP_OR_RETURN(c, hipMemcpyAsync(nd.as<uint8_t>() + (size_t)g.der_words * 4 * k,
+                                        c->ring_der.as<uint8_t>() + (size_t)g.der_words * 4 * o, (size_t)g.der_words * 4,
+                                        hipMemcpyDeviceToDevice, c->stream));
+        c->ring_order[k] = (int)k;
+    }
+    HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
+    if (c->ring_pyr.p) (void)hipFree(c->ring_pyr.p);
+    if (c->ring_der.p) (void)hipFree(c->ring_der.p);
+    c->ring_pyr = np;
+    c->ring_der = nd;
+    c->ring_cap = cap;
+    return MDX_OK;
+}
+
+extern "C" int mdx_ring_reset(mdx_ctx* c)
+{
+    if (!c) return MDX_EINVAL;
+    c->ring_order.clear();
+    return MDX_OK;
+}
+
+extern "C" int mdx_ring_push(mdx_ctx* c, const uint8_t* img, int w, int h, int stride, int fmt, int keep)
+{
+    if (!c) return MDX_EINVAL;
+    if (!img) return set_err(c, MDX_EINVAL, "mdx_ring_push: null frame");
+    if (keep < 1) return set_err(c, MDX_EINVAL, "mdx_ring_push: keep must be >= 1");
+    int rc = check_frame(c, "mdx_ring_push", w, h, stride, fmt);
+    if (rc != MDX_OK) return rc;
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    if (w != c->ring_w || h != c->ring_h || c->prm.max_level != c->ring_ml) {   // another geometry: start over
+        c->ring_order.clear();
+        if (c->ring_pyr.p) (void)hipStreamSynchronize(c->stream);
+        if (c->ring_pyr.p) (void)hipFree(c->ring_pyr.p);
+        if (c->ring_der.p) (void)hipFree(c->ring_der.p);
+        c->ring_pyr = DevBuf{};
+        c->ring_der = DevBuf{};
+        c->ring_cap = 0;
+        c->ring_w = w;
+        c->ring_h = h;
+        c->ring_ml = c->prm.max_level;
+    }
+    const Geometry g = make_geometry(w, h, c->prm.max_level);
+    const int n = (int)c->ring_order.size();
+    if ((rc = ring_grow(c, g, std::max(n + 1, std::max(keep, 4)))) != MDX_OK) return rc;
+    // a free slot: the lowest one no held frame uses
+    std::vector<char> used(c->ring_cap, 0);
+    for (int o : c->ring_order) used[o] = 1;
+    int slot = 0;
+    while (used[slot]) slot++;
+    const size_t fbytes = (size_t)stride * h;
+    if ((rc = ensure(c, c->rin, fbytes)) != MDX_OK) return rc;
+    hipStream_t s = c->stream;
+    HIP_OR_RETURN(c, hipMemcpyAsync(c->rin.p, img, fbytes, hipMemcpyHostToDevice, s));
+    uint8_t* pyr = c->ring_pyr.as<uint8_t>() + (size_t)g.img_bytes * slot;
+    uint32_t* der = c->ring_der.as<uint32_t>() + (size_t)g.der_words * slot;
+    HIP_OR_RETURN(c, launch_front(s, 1, c->rin.as<uint8_t>(), c->rin.as<uint8_t>(), w, h, stride, (long long)fbytes, fmt,
+                                  pyr, pyr, g, 1));
+    HIP_OR_RETURN(c, launch_pyr_levels(s, 1, pyr, pyr, g, 1));
+    for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, 1, pyr, der, g, l));
+    c->ring_order.push_back(slot);
+    while ((int)c->ring_order.size() > keep) c->ring_order.erase(c->ring_order.begin());
+    return (int)c->ring_order.size();
+}
+
+extern "C" int mdx_ring_trajectory(mdx_ctx* c, float* traj, int32_t* traj_len, float* start_pts, double* vectors,
+                                   int* num_vectors)
+{
+    if (!c) return MDX_EINVAL;
+    const int nimg = (int)c->ring_order.size();
+    if (nimg < 2) return set_err(c, MDX_EINVAL, "mdx_ring_trajectory: the ring holds %d frame(s), need >= 2", nimg);
+    if (c->prm.max_level != c->ring_ml)
+        return set_err(c, MDX_EINVAL, "mdx_ring_trajectory: max_level changed since the frames were pushed");
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    const Geometry g = make_geometry(c->ring_w, c->ring_h, c->prm.max_level);
+    std::vector<const uint8_t*> fp(nimg);
+    std::vector<const uint32_t*> fd(nimg);
+    for (int j = 0; j < nimg; j++) {
+        fp[j] = c->ring_pyr.as<uint8_t>() + (size_t)g.img_bytes * c->ring_order[j];
+        fd[j] = c->ring_der.as<uint32_t>() + (size_t)g.der_words * c->ring_order[j];
+    }
+    return trajectory_passes(c, g, nimg, c->ring_w, c->ring_h, fp.data(), fd.data(), traj, traj_len, start_pts, vectors,
+                             num_vectors);
 }
 
 // glibc rand() (random_r TYPE_3), the generator of fitSubspace's samples

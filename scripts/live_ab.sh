@@ -1,16 +1,14 @@
 #!/bin/bash
-# GPU box: live-leg (trajectory + fitSubspace) timing of library variants.
-# Usage: bash scripts/live_ab.sh default w5 ...  (see scripts/lib_ab.sh for the naming)
-out=gpurun_out/live_ab; mkdir -p $out
-i=0
-for v in "$@"; do
-    i=$((i+1))
-    lib=$PWD/motion_detection_amd/lib/libmdx_$v.so
-    [ "$v" = default ] && lib=$PWD/motion_detection_amd/lib/libmdx.so
-    MDX_LIB_PATH=$lib timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu --no-roofline --no-4k \
-        > $out/${i}_$v.json 2> $out/${i}_$v.err
-    rc=$?
-    python3 -c "import json; d=json.load(open('$out/${i}_$v.json')); print('$v', d['live_path']['trajectory_ms'])" \
-        || echo "$v rc=$rc"
-    [ $rc -le 1 ] || exit $rc
+# Live-chain leg only (5 x 1080p rgb8 trajectory + fitSubspace), alternating env settings.
+# Usage (GPU box): ROUNDS=2 bash scripts/live_ab.sh "MDX_LK_PTS=0" "MDX_LK_PTS=1"
+mkdir -p gpurun_out/live
+for r in $(seq 1 ${ROUNDS:-2}); do
+    for e in "$@"; do
+        env $e timeout -k 10 120 python3 -c "
+import sys, json; sys.path.insert(0, '.')
+import bench
+print(json.dumps(bench.live_leg(0, 1920, 1080, 16, with_cpu=False, reps=${REPS:-10})))" > gpurun_out/live/out.json 2> gpurun_out/live/err.log
+        rc=$?; [ $rc -eq 0 ] || { echo "$e rc=$rc"; tail -5 gpurun_out/live/err.log; exit $rc; }
+        python3 -c "import json; d=json.load(open('gpurun_out/live/out.json')); print('$e round $r: ring callback', d['trajectory_ms'], 'ms, list', d['trajectory_list_ms'], 'ms, fit_subspace', d['fit_subspace_ms'], 'ms, ring==list', d['ring_equals_list'])"
+    done
 done
