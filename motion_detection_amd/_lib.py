@@ -40,7 +40,7 @@ EXPORTED = [
 ]
 
 # csrc/Makefile STAMPED: the files whose bytes the library's provenance stamp hashes, in order
-STAMPED = ["Makefile", "mdx_internal.h", "mdx_api.cpp", "mdx_kernels.hip", "mdx_lk.hip", "mdx_lkpt.hip", "mdx_warp.hip",
+STAMPED = ["Makefile", "mdx_internal.h", "mdx_api.cpp", "mdx_kernels.hip", "mdx_lk.hip", "mdx_warp.hip",
            "mdx_subspace.hip", "synth.cpp", os.path.join("..", "..", "include", "mdx.h")]
 
 

@@ -44,7 +44,6 @@ struct mdx_ctx {
     int ring_cap = 0, ring_w = 0, ring_h = 0, ring_ml = -1;
     bool lk_debug = false;
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
-    bool lk_pts = false;                     // arbitrary start points: k_lk (MDX_LK_PTS=1: k_lk_pts)
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
     int lk_sub = 0;                          // > 0: LK sub-batch cap (MDX_LK_SUB, tests)
     int plan_w = -1, plan_h = -1, plan_ps = -1, plan_ml = -1, plan_gy0 = -1, plan_gy1 = -1;
@@ -320,7 +319,6 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     if (const char* e = std::getenv("MDX_LK_IMPL")) c->lk_impl = std::atoi(e) == 1 ? 1 : 2;
     if (const char* e = std::getenv("MDX_LK_G")) c->lk_g = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_SUB")) c->lk_sub = std::atoi(e);
-    if (const char* e = std::getenv("MDX_LK_PTS")) c->lk_pts = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         g_create_err = "hipStreamCreate failed";
@@ -476,7 +474,7 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
         if (!have_scharr)
             for (int l = 0; l < g.nlev; l++)
                 HIP_OR_RETURN(c, launch_scharr(s, batch, a.pyr1, const_cast<uint32_t*>(a.der), g, l));
-        HIP_OR_RETURN(c, c->lk_pts ? launch_lk_pts(s, batch, a) : launch_lk(s, batch, a));
+        HIP_OR_RETURN(c, launch_lk(s, batch, a));
         return MDX_OK;
     }
     a.plan = c->plan;

@@ -1,3 +1,9 @@
+// EXPERIMENT (not built; measured slower than k_lk).  Was
+// motion_detection_amd/csrc/mdx_lkpt.hip, launched instead of k_lk with MDX_LK_PTS=1; bit-exact in
+// tests/test_trajectory.py and tests/test_ring.py.  Live callback (5 x 1080p rgb8, ring): k_lk 3.96 ms;
+// this kernel 7.40 (8 points / 512 lanes), 5.85 (4 / 256), 6.38 (2 / 128) ms: the chain-summing wave's
+// barriers leave the SIMDs waiting (SQ_WAIT_ANY 72% of wave cycles, VALU 41% busy vs k_lk's 97%).
+//
 // mdx_lkpt.hip -- pyramidal Lucas-Kanade for arbitrary start points (reference row A5 as run by
 // calculateOpticalFlowTrajectory, optical_flow_calculator.cpp:172, on the points the previous pass
 // left: the node's live chain, motion_detection_node.cpp:94-110; also sparse grids whose class
@@ -34,8 +40,14 @@ namespace {
 typedef short s2p __attribute__((ext_vector_type(2)));
 typedef float f2p __attribute__((ext_vector_type(2)));
 
-constexpr int kNP = 8;                 // points per workgroup
-constexpr int kWG = 512;               // lanes per workgroup (8 waves)
+#ifndef LKPT_NP
+#define LKPT_NP 4
+#endif
+#ifndef LKPT_W
+#define LKPT_W 4                       // waves per SIMD the register budget is sized for
+#endif
+constexpr int kNP = LKPT_NP;           // points per workgroup (one wave each)
+constexpr int kWG = 64 * kNP;          // lanes per workgroup
 constexpr int kTPP = kWG / kNP;        // lanes per point (64)
 constexpr int kRC = 8;                 // window rows per chunk
 constexpr int kNCH = kWin / kRC;       // chunks (5)
@@ -78,7 +90,7 @@ struct LkPtShared {
 
 // grid: x -> 8 consecutive points, y -> pair.  Start points from a.prev_pts (trajectory passes,
 // flags 0: nextPt = prevPt) or the pixel_step grid.
-__global__ __launch_bounds__(512, 4) void k_lk_pts(LkArgs a)
+__global__ __launch_bounds__(64 * LKPT_NP, LKPT_W) void k_lk_pts(LkArgs a)
 {
     constexpr float HALFW = 19.5f;             // (winSize.width-1)*0.5f
     constexpr float FLT_SCALE = 1.f / (1 << 20);
@@ -184,7 +196,7 @@ __global__ __launch_bounds__(512, 4) void k_lk_pts(LkArgs a)
                 *(lfl)(uintptr_t)((m < 4 ? pc0 : pc4) + 4u * ((uint32_t)(b * kNP * 4 * kPS1) + mo)) = fx * fy;
             }
             __syncthreads();
-            if (wave == ((c + rot) & 7)) {
+            if (wave == ((c + rot) % kNP) && sp < kNP) {
                 // lanes sq < 4: the (A11, A22) chain sq of point sp; sq >= 4: its A12 chain sq - 4
                 if (sq < 4) {
                     f2p acc = c ? sh.acc2[sp][sq] : f2p{0.f, 0.f};
@@ -302,7 +314,7 @@ __global__ __launch_bounds__(512, 4) void k_lk_pts(LkArgs a)
                     *((lf2)(uintptr_t)((m < 4 ? pb0 : pb4) + 8u * (uint32_t)(b * kNP * 4 * kPS2 + (m < 4 ? m * 20 : 0)))) = f * fd;
                 }
                 __syncthreads();
-                if (wave == ((c + rot) & 7) && sq < 4) {
+                if (wave == ((c + rot) % kNP) && sp < kNP && sq < 4) {
                     f2p acc = c ? sh.acc2[sp][sq] : f2p{0.f, 0.f};
                     const f2p* src = sh.pab[b][sp][sq];
 #pragma unroll 1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Live-chain leg only (5 x 1080p rgb8 trajectory + fitSubspace), alternating env settings.
-# Usage (GPU box): ROUNDS=2 bash scripts/live_ab.sh "MDX_LK_PTS=0" "MDX_LK_PTS=1"
+# Usage (GPU box): ROUNDS=2 bash scripts/live_ab.sh "MDX_LK_AUX=1" "MDX_LK_AUX=0"
 mkdir -p gpurun_out/live
 for r in $(seq 1 ${ROUNDS:-2}); do
     for e in "$@"; do
