@@ -312,7 +312,7 @@ def main_c4(args, D: Dist, threads: int):
 
     def exchange(c, d):
         rec = np.empty(per_rank * 96, np.uint8)
-        c.d2h(rec, d["cand"])                                    # synchronous: this frame's flow is done
+        c.d2h(rec, d["cand"])                                    # the stream is drained: a plain copy
         local = rec.tobytes()[:96 * len(mine)] + pad * (per_rank - len(mine))
         parts = D.allgather_bytes(local)
         allrec = bytearray(K * 96)
@@ -327,20 +327,23 @@ def main_c4(args, D: Dist, threads: int):
             for j, k in enumerate(mine):
                 c.band_flow_dev(d["i1"], d["i2"], w, h, w * 3, fmt, *rows[k], d["np"], d["st"], d["cand"] + 96 * j)
         t1 = time.perf_counter()
-        tx = 0.0
+        tx = tw = 0.0
         for c, d in zip(ctxs, bufs):                             # then, frame by frame: records, fit, warp
             e0 = time.perf_counter()
+            c.sync()                                             # this frame's flow (its stream) is done
+            e1 = time.perf_counter()
             exchange(c, d)
-            tx += time.perf_counter() - e0
+            tw += e1 - e0
+            tx += time.perf_counter() - e1
             for k in mine:
                 c.band_fit_warp_dev(K, d["cands"], *rows[k], d["mask"] + rows[k][0] * w, 0, d["num"])
         for c in ctxs:
             c.sync()
         t3 = time.perf_counter()
         if timed:
-            t_ph["flow"] += t1 - t0
-            t_ph["exchange"] += tx
-            t_ph["fit_warp"] += t3 - t1 - tx
+            t_ph["flow"] += t1 - t0 + tw                         # launches + waits for the flow streams
+            t_ph["exchange"] += tx                               # record d2h + all-gather + h2d only
+            t_ph["fit_warp"] += t3 - t1 - tx - tw
 
     for _ in range(args.warmup):
         step()

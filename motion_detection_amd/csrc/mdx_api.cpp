@@ -498,6 +498,28 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
     return MDX_OK;
 }
 
+// Row-band mode: the previous frame's (pyr1) core rows a band's class planes read at each level --
+// padded rows [vlo - 1, vhi + 2) of the planes' source (k_lk_class_fused reads y-1 .. y+2, the
+// Scharr planes behind k_lk_class the same), reflect-101 border rows folded onto the core rows they
+// mirror -- and the rows the next level's pyrDown reads from it (pyramids.cpp: dst row r reads rows
+// 2r-2 .. 2r+2).  Only those rows of pyr1 are built; the next frame's pyramid stays whole, since J
+// may be read anywhere in it.
+static void band_rows(const Geometry& g, const ClassPlan& P, RowSpan* rows)
+{
+    for (int l = g.nlev - 1; l >= 0; l--) {
+        const int h = g.lv[l].h;
+        const int lo = P.lv[l].vlo - 1 - kPad, hi = P.lv[l].vhi + 2 - kPad;   // core coordinates
+        int clo = std::max(lo, 0), chi = std::min(hi, h);
+        if (lo < 0) chi = std::max(chi, std::min(h, 1 - lo));                 // rows lo..-1 mirror 1..-lo
+        if (hi > h) clo = std::min(clo, std::max(0, 2 * h - 1 - hi));         // rows h..hi-1 mirror down to 2h-1-hi
+        if (l + 1 < g.nlev) {
+            clo = std::min(clo, std::max(0, 2 * rows[l + 1].lo - 2));
+            chi = std::max(chi, std::min(h, 2 * rows[l + 1].hi + 2));
+        }
+        rows[l] = RowSpan{clo, std::max(clo, chi)};
+    }
+}
+
 // The pipeline on device buffers.  d_np/d_st must be valid (LK writes them).
 // Row-band mode (cand != null, batch 1): LK and classification for grid rows [gy0, gy1) only, the
 // band's record to *cand, no fit and no mask.
@@ -533,10 +555,20 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
     // = gray + pad + level 1 of the first frames (k_front), "pyrdown" = the rest of the pyramids.
     hipEvent_t prev_ready = nullptr;
     const long long fs = (long long)frame_stride;
+    // a row band (batch 1): the rows of the previous frame's pyramid its class planes read
+    RowSpan rows[kMaxLevels];
+    const RowSpan* prows = nullptr;
+    if (cand && c->lk_impl == 2 && npts > 0 && nyb > 0 && nyb < ny) {
+        if ((rc = ensure_class_plan(c, g, w, h, P.pixel_step, batch, gy0, gy1)) != MDX_OK) return rc;
+        if (c->plan.nch != 0) {
+            band_rows(g, c->plan, rows);
+            prows = rows;
+        }
+    }
     if (c->aux && c->lk_impl == 2) {
-        HIP_OR_RETURN(c, launch_front(s, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g, 1));
+        HIP_OR_RETURN(c, launch_front(s, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g, 1, prows));
         mark(c, 1);
-        HIP_OR_RETURN(c, launch_pyr_levels(s, batch, pyr1, pyr2, g, 1));
+        HIP_OR_RETURN(c, launch_pyr_levels(s, batch, pyr1, pyr2, g, 1, prows));
         HIP_OR_RETURN(c, hipEventRecord(c->lkev[kMaxLevels + 1], s));
         prev_ready = c->lkev[kMaxLevels + 1];
         HIP_OR_RETURN(c, launch_front(s, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g, 2));

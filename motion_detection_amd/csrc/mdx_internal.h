@@ -107,6 +107,11 @@ struct LkArgs {
     int dbg_pt;              // point whose per-iteration values are appended after dbg (pair 0)
 };
 
+// Core rows [lo, hi) of one pyramid level (row-band mode: what a band's LK reads)
+struct RowSpan {
+    int lo, hi;
+};
+
 // Launchers (mdx_kernels.hip).  All enqueue on `s`.
 // fsel: 0 both frames of every pair, 1 the first frame only, 2 the second frame only
 hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const uint8_t* in2, int w, int h,
@@ -114,11 +119,15 @@ hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const u
                            const Geometry& g, int fsel = 0);
 // gray + pad of level 0 and pyrDown to level 1 in one pass (k_front; launch_gray_pad when nlev == 1);
 // launch_pyr_levels then builds levels 2 .. nlev-1 (k_front in level mode, one launch per level)
+// rows (may be null = all): [nlev] core rows wanted per level; only the bands covering them are built
 hipError_t launch_front(hipStream_t s, int batch, const uint8_t* in1, const uint8_t* in2, int w, int h, int stride,
                         long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g,
-                        int fsel = 0);
-hipError_t launch_pyr_levels(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int fsel = 0);
-hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level);
+                        int fsel = 0, const RowSpan* rows = nullptr);
+hipError_t launch_pyr_levels(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int fsel = 0,
+                             const RowSpan* rows = nullptr);
+// padded rows [prow0, prow1) of the level's derivative planes (default: all)
+hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level,
+                         int prow0 = 0, int prow1 = -1);
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
 // Trajectory subspace RANSAC (fitSubspace): mean-subtracted data, nhyp hypotheses of d columns
 // (cols: [nhyp][d]), winner's residuals / outlier flags; best[0] = winner or -1.  Scratch: data

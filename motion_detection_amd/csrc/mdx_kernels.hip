@@ -17,6 +17,8 @@
 #include <float.h>
 #include <limits.h>
 
+#include <algorithm>
+
 namespace mdx {
 
 __device__ __forceinline__ int r101(int p, int len)
@@ -135,6 +137,7 @@ struct FrontArgs {
     const uint8_t* in1;
     const uint8_t* in2;
     int w, h, stride, fmt, fsel, nbands, nz;
+    int band0;       // first band of the launch (row-band mode builds only the bands a band's LK reads)
     long long frame_stride, img_bytes;
     uint8_t* pyr1;
     uint8_t* pyr2;
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(256) void k_front(FrontArgs a)
     const int nb = gridDim.x;
     int task = blockIdx.x;
     if ((nb & 7) == 0) task = (blockIdx.x & 7) * (nb >> 3) + (blockIdx.x >> 3);
-    const int band = task % a.nbands, z = task / a.nbands;
+    const int band = a.band0 + task % a.nbands, z = task / a.nbands;
     const int which = a.fsel ? a.fsel - 1 : z & 1, pair = a.fsel ? z : z >> 1;
     const int w = a.w, h = a.h, w1 = a.L1.w, h1 = a.L1.h;
     const int Y0 = band * RB, e1 = min(Y0 + RB, h1), r0 = 2 * Y0, e0 = min(2 * Y0 + 2 * RB, h);
@@ -413,11 +416,12 @@ __global__ __launch_bounds__(256) void k_front(FrontArgs a)
 // (copyMakeBorder ... BORDER_CONSTANT).  Per thread 4 pixels (one 16-B store); each of the
 // three source rows is one dwordx3 load of bytes x0-4 .. x0+7.
 __global__ __launch_bounds__(256) void k_scharr(const uint8_t* __restrict__ pyr1, uint32_t* __restrict__ der,
-                                                long long img_bytes, long long der_words, Level L, int nchunk)
+                                                long long img_bytes, long long der_words, Level L, int nchunk,
+                                                int prow0)
 {
     const int pair = blockIdx.z;
     const int c = blockIdx.x * blockDim.x + threadIdx.x + 4;         // word chunks 0..3 are margin
-    const int py = blockIdx.y - kPad;
+    const int py = prow0 + blockIdx.y - kPad;                        // padded rows prow0 + blockIdx.y
     if (c > nchunk) return;
     const int px0 = 4 * c - kXOff;
     uint32_t o[4] = {0, 0, 0, 0};
@@ -1134,7 +1138,7 @@ hipError_t launch_gray_pad(hipStream_t s, int batch, const uint8_t* in1, const u
 // k_front's band height: 4 destination rows at 1080p (27 KB of LDS, 5-6 bands per CU): one frame
 // side of gray + pad + level 1 takes 44 us there against 56 with 8 rows and 107 for the earlier
 // k_gray_pad + k_pyrdown (scripts/micro/front_bench.hip).
-static hipError_t launch_front_bands(hipStream_t s, FrontArgs& a, int mode)
+static hipError_t launch_front_bands(hipStream_t s, FrontArgs& a, int mode, int rlo = 0, int rhi = -1)
 {
     // the band height: 4 destination rows while a band's LDS fits 32 KB, else 2 (8K frames: 62 KB),
     // else 1; beyond 64 KB (rows wider than ~8.7K px at RB = 1) the launch asks for the larger
@@ -1145,7 +1149,12 @@ static hipError_t launch_front_bands(hipStream_t s, FrontArgs& a, int mode)
     // k_front's static arrays (out0, out1, nout) share the CU's 160 KB with the dynamic rows
     const size_t lds_static = (size_t)(2 * rb + 80 + rb + 80 + 2) * sizeof(int);
     if (lds + lds_static > 160 * 1024) return hipErrorInvalidValue;   // rows wider than ~31K px
-    a.nbands = (a.L1.h + rb - 1) / rb;
+    // destination rows [rlo, rhi) of the level built (all by default): the bands covering them
+    if (rhi < 0 || rhi > a.L1.h) rhi = a.L1.h;
+    rlo = std::max(0, std::min(rlo, rhi));
+    a.band0 = rlo / rb;
+    a.nbands = (rhi + rb - 1) / rb - a.band0;
+    if (a.nbands <= 0) return hipSuccess;
     const dim3 grid((unsigned)(a.nbands * a.nz));
 #define MDX_FRONT_CASE(M, R)                                                                             \
     if (mode == M && rb == R) {                                                                          \
@@ -1182,7 +1191,8 @@ static FrontArgs front_args(int batch, uint8_t* pyr1, uint8_t* pyr2, const Geome
 }
 
 hipError_t launch_front(hipStream_t s, int batch, const uint8_t* in1, const uint8_t* in2, int w, int h, int stride,
-                        long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int fsel)
+                        long long frame_stride, int fmt, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int fsel,
+                        const RowSpan* rows)
 {
     if (g.nlev < 2) return launch_gray_pad(s, batch, in1, in2, w, h, stride, frame_stride, fmt, pyr1, pyr2, g, fsel);
     FrontArgs a = front_args(batch, pyr1, pyr2, g, 0, fsel);
@@ -1192,24 +1202,35 @@ hipError_t launch_front(hipStream_t s, int batch, const uint8_t* in1, const uint
     a.fmt = fmt;
     a.frame_stride = frame_stride;
     a.aligned = ((((uintptr_t)in1 | (uintptr_t)in2) & 3) == 0 && (stride & 3) == 0 && (frame_stride & 3) == 0) ? 1 : 0;
-    return launch_front_bands(s, a, fmt == MDX_FMT_GRAY8 ? 0 : 1);
+    // level-1 rows: those wanted at level 1 and those whose bands write the wanted level-0 rows
+    int r1lo = 0, r1hi = -1;
+    if (rows) {
+        r1lo = std::min(rows[1].lo, rows[0].lo / 2);
+        r1hi = std::max(rows[1].hi, (rows[0].hi + 1) / 2);
+    }
+    return launch_front_bands(s, a, fmt == MDX_FMT_GRAY8 ? 0 : 1, r1lo, r1hi);
 }
 
-hipError_t launch_pyr_levels(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int fsel)
+hipError_t launch_pyr_levels(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int fsel,
+                             const RowSpan* rows)
 {
     for (int l = 2; l < g.nlev; l++) {
         FrontArgs a = front_args(batch, pyr1, pyr2, g, l - 1, fsel);
-        if (hipError_t e = launch_front_bands(s, a, 2)) return e;
+        if (hipError_t e = launch_front_bands(s, a, 2, rows ? rows[l].lo : 0, rows ? rows[l].hi : -1)) return e;
     }
     return hipSuccess;
 }
 
-hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level)
+hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level,
+                         int prow0, int prow1)
 {
     const Level& L = g.lv[level];
     const int nchunk = (kXOff + L.w + kPad - 1) / 4;                 // last 4-word chunk
-    const dim3 grid((nchunk - 4 + 1 + 63) / 64, L.h + 2 * kPad, batch);
-    hipLaunchKernelGGL(k_scharr, grid, dim3(64), 0, s, pyr1, der, g.img_bytes, g.der_words, L, nchunk);
+    if (prow1 < 0 || prow1 > L.rows) prow1 = L.rows;
+    prow0 = std::max(0, std::min(prow0, prow1));
+    if (prow1 == prow0) return hipSuccess;
+    const dim3 grid((nchunk - 4 + 1 + 63) / 64, prow1 - prow0, batch);
+    hipLaunchKernelGGL(k_scharr, grid, dim3(64), 0, s, pyr1, der, g.img_bytes, g.der_words, L, nchunk, prow0);
     return hipGetLastError();
 }
 

@@ -122,6 +122,15 @@ __device__ __forceinline__ void lk_vmcnt0()
     __builtin_amdgcn_s_waitcnt(0x0F70);
     __builtin_amdgcn_sched_barrier(0);
 }
+// s_waitcnt vmcnt(N), N < 16
+template <int N>
+__device__ __forceinline__ void lk_vmcnt()
+{
+    static_assert(N >= 0 && N < 16, "vmcnt field");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0F70 | N);
+    __builtin_amdgcn_sched_barrier(0);
+}
 
 // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs; remap so that each
 // XCD gets a contiguous range of waves (= a contiguous image band), whose class planes then
@@ -581,8 +590,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
     constexpr float HALFW = 19.5f;
     constexpr float FLT_SCALE = 1.f / (1 << 20);
     constexpr int UB = S * UW;                                    // (D, C) pairs per union buffer
-    __shared__ __attribute__((aligned(16))) uint32_t dU[2][2 * UB];   // [buf][slot][UW][D, C]
-    __shared__ __attribute__((aligned(16))) uint32_t dJ[2][256];      // [buf][quad][16]
+#ifdef MDX_LK_DMA3
+    constexpr int NB = 3;                                         // rows fetched two ahead
+#else
+    constexpr int NB = 2;
+#endif
+    __shared__ __attribute__((aligned(16))) uint32_t dU[NB][2 * UB];   // [buf][slot][UW][D, C]
+    __shared__ __attribute__((aligned(16))) uint32_t dJ[NB][256];      // [buf][quad][16]
 
     const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
     const unsigned long long smask = ((1ull << LPS) - 1) << (slot * LPS);
@@ -735,6 +749,57 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
         lds_u2v* lE = (lds_u2v*)&dU[0][2 * (slot * UW + q.off + k)];
         // taps of the current window row (pa) are the previous row's lower taps (pb)
         s2 pa[10], pb[10];
+#ifdef MDX_LK_DMA3
+        // three buffers each, rows fetched two ahead: union row r and J row r live in buffer r % 3,
+        // and row y waits only for what row y-2 issued (vmcnt = the ND + 1 loads of row y-1)
+        dma_union(0);
+        dma_j(0);
+        dma_j(1);
+        dma_union(1);
+        dma_j(2);
+        lk_vmcnt<ND + 1>();
+        {
+            uint32_t rj[11];
+            read_j(0, rj);
+#pragma unroll
+            for (int gi = 0; gi < 10; gi++) pa[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
+        }
+        auto row = [&](int y, int bu, s2 (&up)[10], s2 (&lo)[10]) {
+            if (y) {
+                if (y + 1 < kWin) lk_vmcnt<ND + 1>();                 // union row y, J row y+1
+                else lk_vmcnt0();
+            }
+            // buffer (y + 2) % 3 held union row y-1 and J row y-1 (J row y+3 goes to buffer y % 3,
+            // whose J row y the previous row consumed)
+            const int b2 = bu == 0 ? 2 : bu - 1;
+            if (y + 2 < kWin) dma_union(b2);
+            if (y + 3 <= kWin) dma_j(bu);
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t rj[11];
+            const int b1 = bu == 2 ? 0 : bu + 1;
+            read_j(b1, rj);
+            lds_u2v* lEb = lE + bu * UB;
+#pragma unroll
+            for (int gi = 0; gi < 10; gi++) {
+                const v2u dc = lEb[4 * gi];
+                lo[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
+                const int jd = __builtin_amdgcn_sdot2(up[gi], W0, __builtin_amdgcn_sdot2(lo[gi], W1, (int)dc.y, false),
+                                                      false) >> 9;
+                const float fd = (float)jd;
+                const f2 f = {(float)(int16_t)dc.x, (float)((int)dc.x >> 16)};
+                acc = acc + f * fd;
+            }
+            asm volatile("" : "+v"(acc));
+        };
+        int bu = 0;
+#pragma unroll 1
+        for (int y = 0; y < kWin; y += 2) {
+            row(y, bu, pa, pb);
+            bu = bu == 2 ? 0 : bu + 1;
+            row(y + 1, bu, pb, pa);
+            bu = bu == 2 ? 0 : bu + 1;
+        }
+#else
         dma_union(0);
         dma_j(0);
         dma_j(1);
@@ -775,6 +840,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
             row(y, std::integral_constant<int, 0>{}, pa, pb);
             row(y + 1, std::integral_constant<int, 1>{}, pb, pa);
         }
+#endif
         if (!act) acc = f2{0.f, 0.f};
         // b = (P0+P2) + (P1+P3) across the quad; inactive quads compute values they ignore
         const float b1s = (quad_bcast<0>(acc.x) + quad_bcast<2>(acc.x)) + (quad_bcast<1>(acc.x) + quad_bcast<3>(acc.x));
@@ -917,7 +983,9 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
                 const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.vhi - C.vlo, nb * C.nrx * C.nry);
                 // this level's Scharr planes (the caller left them to us): on the aux stream, so
                 // they too run while the coarser levels iterate
-                if (hipError_t e = launch_scharr(sa, nb, b.pyr1, const_cast<uint32_t*>(b.der), a.g, l)) return e;
+                // (the derivative rows the class planes read: v, v + 1 for plane rows v in [vlo, vhi))
+                if (hipError_t e = launch_scharr(sa, nb, b.pyr1, const_cast<uint32_t*>(b.der), a.g, l, C.vlo, C.vhi + 1))
+                    return e;
                 hipLaunchKernelGGL(k_lk_class, grid, dim3(64), 0, sa, b.pyr1, b.der, bcls, ca);
             }
             float4* bA = Ab + ((long long)l * batch + p) * a.npts;

@@ -34,6 +34,11 @@ def mdx():
     """The in-tree libmdx.so, rebuilt from the tree (make -B) whenever it is missing or its stamp
     does not match the sources here, so a test never runs a library built from other sources."""
     import motion_detection_amd as m
+    if os.environ.get("MDX_LIB_PATH"):
+        # an explicitly chosen library (scripts/build_variant.sh A/B runs: this tree's sources
+        # with extra -D flags, so its stamp differs by construction)
+        m.lib()
+        return m
     if not os.path.exists(m.LIB_PATH) or _lib_stamp(m.LIB_PATH) != m._lib.source_sha256():
         m.build()
     m.lib()
