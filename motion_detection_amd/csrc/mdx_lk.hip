@@ -108,7 +108,16 @@ __device__ __forceinline__ void wave_lds_fence()
 }
 
 // k_lk_iter: 5 waves/SIMD (<= 102 VGPRs; measured 3% faster than 6 at <= 80)
-constexpr int kLkIterWavesPerEU = 5;
+#ifndef MDX_LK_WPE
+#define MDX_LK_WPE 4
+#endif
+#ifndef MDX_LK_NB
+#define MDX_LK_NB 2
+#endif
+#ifndef MDX_LK_RFIRST
+#define MDX_LK_RFIRST 0
+#endif
+constexpr int kLkIterWavesPerEU = MDX_LK_WPE;
 typedef __attribute__((address_space(3))) void* lds_ptr;
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 // volatile LDS views: each access stays one ds_read_b64 / ds_read_b128 (never merged into a
@@ -130,6 +139,16 @@ __device__ __forceinline__ void lk_vmcnt()
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(0x0F70 | N);
     __builtin_amdgcn_sched_barrier(0);
+}
+
+// compile-time loop: f(integral_constant<I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f)
+{
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
 }
 
 // XCD-aware block order: blocks are dealt round-robin over the 8 XCDs; remap so that each
@@ -390,8 +409,12 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
     constexpr int LPS = Sh::LPS, S = Sh::S, ND = Sh::ND;
     constexpr int NB = 3;                                          // row images: NB - 1 rows in flight ahead
     constexpr float FLT_SCALE = 1.f / (1 << 20);
-    // [buf][slot][UW][D, C]: the wave's union row image, filled by LDS-DMA like k_lk_iter's
-    __shared__ __attribute__((aligned(16))) uint32_t img[NB][ND * 256];
+    // [slot][UW][D, C]: the wave's union row images, filled by LDS-DMA like k_lk_iter's; one
+    // __shared__ array per buffer, so that no compiler wait ties a row's reads to later rows' DMA
+    __shared__ __attribute__((aligned(16))) uint32_t img0[ND * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t img1[ND * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t img2[ND * 256];
+    static_assert(NB == 3, "three row images");
 
     const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
     const int nw = gridDim.x;
@@ -419,38 +442,43 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
             uoff[c] = sp < S ? src : 0x80000000u;
         }
     }
-    auto dma = [&](int b) {
+    auto ibuf = [&](auto bc) -> uint32_t* {
+        constexpr int bb = decltype(bc)::value;
+        if constexpr (bb == 0) return img0;
+        else if constexpr (bb == 1) return img1;
+        else return img2;
+    };
+    auto dma = [&](auto bc) {
+        uint32_t* I = ibuf(bc);
 #pragma unroll
         for (int c = 0; c < ND; c++) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)&img[b][256 * c], 16, (int)uoff[c], 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)(I + 256 * c), 16, (int)uoff[c], 0, 0, 0);
             uoff[c] += rowb;
         }
     };
-    lds_u2v* lE = (lds_u2v*)&img[0][2 * (slot * UW + q.off + k)];
+    const int el = 2 * (slot * UW + q.off + k);
 
     // lane k owns SSE lane k (columns 4g+k), rows in order; ((P0+P1)+P2)+P3 across the quad
     f2 sd = {0.f, 0.f};
     float s12 = 0.f;
     constexpr int PF = NB - 1;                                     // rows in flight ahead
-#pragma unroll
-    for (int y = 0; y < PF; y++) dma(y);
-#pragma unroll
-    for (int y = 0; y < kWin; y++) {
-        const int buf = y % NB;
+    dma(std::integral_constant<int, 0>{});
+    dma(std::integral_constant<int, 1>{});
+    static_for<0, kWin>([&](auto yc) {
+        constexpr int y = decltype(yc)::value;
         // row y has landed once at most the later rows' pieces are outstanding
-        __builtin_amdgcn_sched_barrier(0);
-        const int later = (y + PF - 1 < kWin - 1 ? y + PF - 1 : kWin - 1) - y;
-        if (later >= 3) __builtin_amdgcn_s_waitcnt(0x0F70 | (3 * ND));
-        else if (later == 2) __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * ND));
-        else if (later == 1) __builtin_amdgcn_s_waitcnt(0x0F70 | ND);
-        else __builtin_amdgcn_s_waitcnt(0x0F70);
-        __builtin_amdgcn_sched_barrier(0);
+        constexpr int later = (y + PF - 1 < kWin - 1 ? y + PF - 1 : kWin - 1) - y;
+        lk_vmcnt<later * ND>();
         // row y+PF into the image row y-1 used (its reads were consumed last iteration)
-        if (y + PF < kWin) dma((y + PF) % NB);
+        if constexpr (y + PF < kWin) dma(std::integral_constant<int, (y + PF) % NB>{});
         __builtin_amdgcn_sched_barrier(0);
+        lds_u2v* lE = (lds_u2v*)(ibuf(std::integral_constant<int, y % NB>{}) + el);
+        uint32_t dw[10];
+#pragma unroll
+        for (int gi = 0; gi < 10; gi++) dw[gi] = lE[4 * gi].x;      // the D word of pair q.off + k + 4 gi
 #pragma unroll
         for (int gi = 0; gi < 10; gi++) {
-            const uint32_t d = lE[buf * (ND * 128) + 4 * gi].x;   // the D word of pair q.off + k + 4 gi
+            const uint32_t d = dw[gi];
             const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
             // the reference rounds each product to float, then adds (_mm_mul_ps, _mm_add_ps).
             // |Ix|, |Iy| <= 4080 (Scharr of u8, interpolated), so every product is below 2^24 and
@@ -458,7 +486,7 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
             sd = __builtin_elementwise_fma(f, f, sd);      // (Ix*Ix, Iy*Iy)
             s12 = __builtin_fmaf(f.x, f.y, s12);           // Ix*Iy
         }
-    }
+    });
     const float a11 = ((quad_bcast<0>(sd.x) + quad_bcast<1>(sd.x)) + quad_bcast<2>(sd.x)) + quad_bcast<3>(sd.x);
     const float a12 = ((quad_bcast<0>(s12) + quad_bcast<1>(s12)) + quad_bcast<2>(s12)) + quad_bcast<3>(s12);
     const float a22 = ((quad_bcast<0>(sd.y) + quad_bcast<1>(sd.y)) + quad_bcast<2>(sd.y)) + quad_bcast<3>(sd.y);
@@ -590,13 +618,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
     constexpr float HALFW = 19.5f;
     constexpr float FLT_SCALE = 1.f / (1 << 20);
     constexpr int UB = S * UW;                                    // (D, C) pairs per union buffer
-#ifdef MDX_LK_DMA3
-    constexpr int NB = 3;                                         // rows fetched two ahead
-#else
-    constexpr int NB = 2;
-#endif
-    __shared__ __attribute__((aligned(16))) uint32_t dU[NB][2 * UB];   // [buf][slot][UW][D, C]
-    __shared__ __attribute__((aligned(16))) uint32_t dJ[NB][256];      // [buf][quad][16]
+    // Row buffers: window rows are fetched NB - 1 ahead of the row being summed.  One __shared__
+    // array per buffer, so that the compiler sees a row's LDS reads and the DMA into another
+    // buffer as disjoint: with one [NB][...] array it put a vmcnt(0) -- a wait for the DMA just
+    // issued -- in front of every read that followed a DMA, and no row overlapped its fetch.
+    constexpr int NB = MDX_LK_NB;
+    static_assert(NB == 2 || NB == 3, "row buffers");
+    static_assert(kWin == 40, "row schedule (20 row pairs; 6 row sextets + 4)");
+    __shared__ __attribute__((aligned(16))) uint32_t dU0[2 * UB];   // [slot][UW][D, C]
+    __shared__ __attribute__((aligned(16))) uint32_t dU1[2 * UB];
+    __shared__ __attribute__((aligned(16))) uint32_t dU2[NB > 2 ? 2 * UB : 4];
+    __shared__ __attribute__((aligned(16))) uint32_t dJ0[256];      // [quad][16]
+    __shared__ __attribute__((aligned(16))) uint32_t dJ1[256];
+    __shared__ __attribute__((aligned(16))) uint32_t dJ2[NB > 2 ? 256 : 4];
 
     const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
     const unsigned long long smask = ((1ull << LPS) - 1) << (slot * LPS);
@@ -726,105 +760,90 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                 uoff[c] = (uint32_t)__shfl((int)mine, sp * LPS) + (uint32_t)wb;
             }
         }
-        auto dma_union = [&](int b) {
+        auto ubuf = [&](auto bc) -> uint32_t* {
+            constexpr int bb = decltype(bc)::value;
+            if constexpr (bb == 0) return dU0;
+            else if constexpr (bb == 1) return dU1;
+            else return dU2;
+        };
+        auto jbuf = [&](auto bc) -> uint32_t* {
+            constexpr int bb = decltype(bc)::value;
+            if constexpr (bb == 0) return dJ0;
+            else if constexpr (bb == 1) return dJ1;
+            else return dJ2;
+        };
+        auto dma_union = [&](auto bc) {
+            uint32_t* U = ubuf(bc);
 #pragma unroll
             for (int c = 0; c < ND; c++) {
                 if (c < ND - 1 || 1024 * c + 16 * lane < Sh::BYTES)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)&dU[b][256 * c], 16, (int)uoff[c], 0, 0, 0);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)(U + 256 * c), 16, (int)uoff[c], 0, 0, 0);
                 uoff[c] += rowb;
             }
         };
-        auto dma_j = [&](int b) {
+        auto dma_j = [&](auto bc) {
             // the quad's taps span 44 bytes: lanes 0-2 carry them, lane 3 stays idle
-            if (k < 3) __builtin_amdgcn_raw_ptr_buffer_load_lds(jrs, (lds_ptr)&dJ[b][0], 16, (int)joff, 0, 0, 0);
+            if (k < 3) __builtin_amdgcn_raw_ptr_buffer_load_lds(jrs, (lds_ptr)jbuf(bc), 16, (int)joff, 0, 0, 0);
             joff += (uint32_t)pitch;
         };
-        lds_u4v* lJ = (lds_u4v*)&dJ[0][(lane >> 2) * 16];
-        auto read_j = [&](int b, uint32_t (&rj)[11]) {
-            const v4u j0 = lJ[b * 64], j1 = lJ[b * 64 + 1], j2 = lJ[b * 64 + 2];
+        const int jl = (lane >> 2) * 16, el = 2 * (slot * UW + q.off + k);
+        auto read_j = [&](auto bc, uint32_t (&rj)[11]) {
+            lds_u4v* lJ = (lds_u4v*)(jbuf(bc) + jl);
+            const v4u j0 = lJ[0], j1 = lJ[1], j2 = lJ[2];
             rj[0] = j0.x; rj[1] = j0.y; rj[2] = j0.z; rj[3] = j0.w;
             rj[4] = j1.x; rj[5] = j1.y; rj[6] = j1.z; rj[7] = j1.w;
             rj[8] = j2.x; rj[9] = j2.y; rj[10] = j2.z;
         };
-        lds_u2v* lE = (lds_u2v*)&dU[0][2 * (slot * UW + q.off + k)];
+        // union row r and J row r live in buffer r % NB
+        constexpr int D = NB - 1;
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
         // taps of the current window row (pa) are the previous row's lower taps (pb)
         s2 pa[10], pb[10];
-#ifdef MDX_LK_DMA3
-        // three buffers each, rows fetched two ahead: union row r and J row r live in buffer r % 3,
-        // and row y waits only for what row y-2 issued (vmcnt = the ND + 1 loads of row y-1)
-        dma_union(0);
-        dma_j(0);
-        dma_j(1);
-        dma_union(1);
-        dma_j(2);
-        lk_vmcnt<ND + 1>();
+        dma_union(I0{});
+        dma_j(I0{});
+        dma_j(I1{});
+        if constexpr (D == 2) {
+            dma_union(I1{});
+            dma_j(I2{});
+        }
+        lk_vmcnt<(D - 1) * (ND + 1)>();
         {
             uint32_t rj[11];
-            read_j(0, rj);
+            read_j(I0{}, rj);
 #pragma unroll
             for (int gi = 0; gi < 10; gi++) pa[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
         }
-        auto row = [&](int y, int bu, s2 (&up)[10], s2 (&lo)[10]) {
-            if (y) {
-                if (y + 1 < kWin) lk_vmcnt<ND + 1>();                 // union row y, J row y+1
-                else lk_vmcnt0();
-            }
-            // buffer (y + 2) % 3 held union row y-1 and J row y-1 (J row y+3 goes to buffer y % 3,
-            // whose J row y the previous row consumed)
-            const int b2 = bu == 0 ? 2 : bu - 1;
-            if (y + 2 < kWin) dma_union(b2);
-            if (y + 3 <= kWin) dma_j(bu);
-            __builtin_amdgcn_sched_barrier(0);
+        // row y (y % period = R): wait until union row y and J row y+1 have landed -- the loads
+        // issued for later rows (W of them) may stay in flight -- then fetch union row y+D and J
+        // row y+D+1 into the buffers rows y-1 / y (already summed) used, and sum the row.  An
+        // opaque use of acc pins each row's arithmetic before the next row's wait.
+        auto row = [&](int y, auto Rc, auto Wc, s2 (&up)[10], s2 (&lo)[10]) {
+            constexpr int R = decltype(Rc)::value, W = decltype(Wc)::value;
+            if (y) lk_vmcnt<W>();
+            auto fetch = [&]() {
+                if (y + D < kWin) dma_union(std::integral_constant<int, (R + D) % NB>{});
+                if (y + D + 1 <= kWin) dma_j(std::integral_constant<int, (R + D + 1) % NB>{});
+                __builtin_amdgcn_sched_barrier(0);
+            };
+#if !MDX_LK_RFIRST
+            fetch();
+#endif
+            // the row's LDS reads back to back (their latencies overlap), then the arithmetic
             uint32_t rj[11];
-            const int b1 = bu == 2 ? 0 : bu + 1;
-            read_j(b1, rj);
-            lds_u2v* lEb = lE + bu * UB;
+            read_j(std::integral_constant<int, (R + 1) % NB>{}, rj);
+            lds_u2v* lE = (lds_u2v*)(ubuf(std::integral_constant<int, R % NB>{}) + el);
+            v2u dcs[10];
+#pragma unroll
+            for (int gi = 0; gi < 10; gi++) dcs[gi] = lE[4 * gi];
+#if MDX_LK_RFIRST
+            __builtin_amdgcn_sched_barrier(0);
+            fetch();
+#endif
 #pragma unroll
             for (int gi = 0; gi < 10; gi++) {
-                const v2u dc = lEb[4 * gi];
-                lo[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
-                const int jd = __builtin_amdgcn_sdot2(up[gi], W0, __builtin_amdgcn_sdot2(lo[gi], W1, (int)dc.y, false),
-                                                      false) >> 9;
-                const float fd = (float)jd;
-                const f2 f = {(float)(int16_t)dc.x, (float)((int)dc.x >> 16)};
-                acc = acc + f * fd;
-            }
-            asm volatile("" : "+v"(acc));
-        };
-        int bu = 0;
-#pragma unroll 1
-        for (int y = 0; y < kWin; y += 2) {
-            row(y, bu, pa, pb);
-            bu = bu == 2 ? 0 : bu + 1;
-            row(y + 1, bu, pb, pa);
-            bu = bu == 2 ? 0 : bu + 1;
-        }
-#else
-        dma_union(0);
-        dma_j(0);
-        dma_j(1);
-        lk_vmcnt0();
-        {
-            uint32_t rj[11];
-            read_j(0, rj);
-#pragma unroll
-            for (int gi = 0; gi < 10; gi++) pa[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
-        }
-        // two rows per step with constant buffers; the taps alternate between pa and pb (no
-        // copies), and an opaque use of acc pins each row's arithmetic before the next row's wait
-        auto row = [&](int y, auto bc, s2 (&up)[10], s2 (&lo)[10]) {
-            constexpr int b = decltype(bc)::value;
-            if (y) lk_vmcnt0();                                       // union row y, J row y+1
-            // next rows' DMA right away: it writes the other buffers (union row y-1 / J row y,
-            // both consumed by the previous row), so it overlaps this row's reads and arithmetic
-            if (y + 1 < kWin) dma_union(b ^ 1);
-            if (y + 2 <= kWin) dma_j(b);
-            __builtin_amdgcn_sched_barrier(0);
-            uint32_t rj[11];
-            read_j(b ^ 1, rj);
-#pragma unroll
-            for (int gi = 0; gi < 10; gi++) {
-                const v2u dc = lE[b * UB + 4 * gi];
+                const v2u dc = dcs[gi];
                 lo[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
                 // (J*32 - I*32) exactly as the reference's CV_DESCALE(...) - I
                 const int jd = __builtin_amdgcn_sdot2(up[gi], W0, __builtin_amdgcn_sdot2(lo[gi], W1, (int)dc.y, false),
@@ -835,12 +854,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
             }
             asm volatile("" : "+v"(acc));
         };
+        if constexpr (NB == 2) {
+            using W = std::integral_constant<int, 0>;
 #pragma unroll 1
-        for (int y = 0; y < kWin; y += 2) {
-            row(y, std::integral_constant<int, 0>{}, pa, pb);
-            row(y + 1, std::integral_constant<int, 1>{}, pb, pa);
+            for (int y = 0; y < kWin; y += 2) {
+                row(y, I0{}, W{}, pa, pb);
+                row(y + 1, I1{}, W{}, pb, pa);
+            }
+        } else {
+            using W = std::integral_constant<int, ND + 1>;
+#pragma unroll 1
+            for (int y = 0; y < 36; y += 6) {
+                row(y, I0{}, W{}, pa, pb);
+                row(y + 1, I1{}, W{}, pb, pa);
+                row(y + 2, I2{}, W{}, pa, pb);
+                row(y + 3, std::integral_constant<int, 3>{}, W{}, pb, pa);
+                row(y + 4, std::integral_constant<int, 4>{}, W{}, pa, pb);
+                row(y + 5, std::integral_constant<int, 5>{}, W{}, pb, pa);
+            }
+            row(36, I0{}, W{}, pa, pb);
+            row(37, I1{}, W{}, pb, pa);
+            row(38, I2{}, W{}, pa, pb);
+            row(39, std::integral_constant<int, 3>{}, std::integral_constant<int, 0>{}, pb, pa);
         }
-#endif
         if (!act) acc = f2{0.f, 0.f};
         // b = (P0+P2) + (P1+P3) across the quad; inactive quads compute values they ignore
         const float b1s = (quad_bcast<0>(acc.x) + quad_bcast<2>(acc.x)) + (quad_bcast<1>(acc.x) + quad_bcast<3>(acc.x));
