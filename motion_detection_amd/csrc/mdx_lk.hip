@@ -501,95 +501,6 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
     if (q.valid && k == 0) Ab[(long long)pair * a.npts + q.gx * a.ny + q.gy] = make_float4(A11, A12, A22, Dinv);
 }
 
-// The same sums with the rows loaded to registers (PF rows ahead) and only their D words written
-// to LDS: more VGPRs (66 vs 20), but on an otherwise idle chip faster than the LDS-DMA form,
-// whose chain reads stride over the (D, C) pairs.  Used for the coarsest level, which runs
-// before any iteration launch (beside the second frames' pyramids only); the LDS-DMA form is
-// the one that shares the chip well with k_lk_iter.
-template <int G, int UW>
-__global__ __launch_bounds__(64) void k_lk_A_rows(LkArgs a, const uint8_t* __restrict__ cls, float4* __restrict__ Ab,
-                                                  int* __restrict__ qctr, int level, int ngroups)
-{
-    using Sh = LkShape<G, UW>;
-    constexpr int LPS = Sh::LPS, S = Sh::S, NP = Sh::NP;
-    constexpr int UWP = 2 * LPS * NP;                             // staged pairs per slot row
-    constexpr float FLT_SCALE = 1.f / (1 << 20);
-    __shared__ __attribute__((aligned(16))) uint32_t lds[2][S][UWP];
-
-    const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
-    const int nw = gridDim.x;
-    const int bid = xcd_remap(blockIdx.x + nw * blockIdx.y, nw * gridDim.y);
-    const int pair = bid / nw, w = bid % nw;
-    if (bid == 0 && lane < 8) qctr[level * 8 + lane] = 0;          // k_lk_iter's queue heads
-    const ClassLevel& C = a.plan.lv[level];
-    const Level L = a.g.lv[level];
-    const int g = w * S + slot;
-    const GroupGeom q = group_geom<G, UW>(a, C, level, g < ngroups ? g : -1, sl);
-    bool ok = q.valid && !(q.ipx < -kWin || q.ipx >= L.w || q.ipy < -kWin || q.ipy >= L.h);
-
-    const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cls + (long long)pair * a.plan.bytes_per_pair, a.plan.bytes_per_pair);
-    const uint32_t rowb = (uint32_t)C.PW * 8;
-    uint32_t roff = q.ubase + (uint32_t)q.v0 * rowb + 16u * sl;
-    const uint32_t* lD0 = &lds[0][slot][q.off + k];
-    constexpr int PF = 4;
-    uint4 rq[PF][NP];
-    // whole 16-B loads: a staged row runs up to UWP >= UW pairs (the tail is never read by a
-    // chain; past the plane row it is the next row's data, past the slab the descriptor gives 0)
-    auto gload = [&](uint4 (&rd)[NP]) {
-#pragma unroll
-        for (int c = 0; c < NP; c++) {
-            const v4u t = __builtin_amdgcn_raw_buffer_load_b128(crs, (int)(roff + 16u * LPS * c), 0, 0);
-            rd[c] = make_uint4(t.x, t.y, t.z, t.w);
-        }
-        roff += rowb;
-    };
-    auto lstore = [&](int buf, const uint4 (&rd)[NP]) {   // the D word of each (D, C) pair
-#pragma unroll
-        for (int c = 0; c < NP; c++)
-            *reinterpret_cast<uint2*>(&lds[buf][slot][2 * (LPS * c + sl)]) = make_uint2(rd[c].x, rd[c].z);
-    };
-
-    f2 sd = {0.f, 0.f};
-    float s12 = 0.f;
-    {
-        uint4 r0[NP];
-        gload(r0);
-#pragma unroll
-        for (int i = 0; i < PF; i++) gload(rq[i]);
-        lstore(0, r0);
-    }
-    wave_lds_fence();
-#pragma unroll
-    for (int y = 0; y < kWin; y++) {
-        const int buf = y & 1;
-        const uint32_t* ld = lD0 + buf * (S * UWP);
-#pragma unroll
-        for (int gi = 0; gi < 10; gi++) {
-            const uint32_t d = ld[4 * gi];
-            const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
-            sd = __builtin_elementwise_fma(f, f, sd);      // exact products: see k_lk_A
-            s12 = __builtin_fmaf(f.x, f.y, s12);
-        }
-        if (y + 1 < kWin) {
-            lstore(buf ^ 1, rq[y % PF]);     // row y+1
-            if (y + 1 + PF < kWin) gload(rq[y % PF]);
-        }
-        wave_lds_fence();
-    }
-    const float a11 = ((quad_bcast<0>(sd.x) + quad_bcast<1>(sd.x)) + quad_bcast<2>(sd.x)) + quad_bcast<3>(sd.x);
-    const float a12 = ((quad_bcast<0>(s12) + quad_bcast<1>(s12)) + quad_bcast<2>(s12)) + quad_bcast<3>(s12);
-    const float a22 = ((quad_bcast<0>(sd.y) + quad_bcast<1>(sd.y)) + quad_bcast<2>(sd.y)) + quad_bcast<3>(sd.y);
-    const float A11 = a11 * FLT_SCALE, A12 = a12 * FLT_SCALE, A22 = a22 * FLT_SCALE;
-    float Dinv = 0.f;
-    if (ok) {
-        const float D = A11 * A22 - A12 * A12;
-        const float minEig = (A22 + A11 - __builtin_sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
-                             (float)(2 * kWin * kWin);
-        if (!(minEig < a.min_eig || D < FLT_EPSILON)) Dinv = 1.f / D;
-    }
-    if (q.valid && k == 0) Ab[(long long)pair * a.npts + q.gx * a.ny + q.gy] = make_float4(A11, A12, A22, Dinv);
-}
-
 // ---- Newton iterations.  grid: x -> persistent wave (a multiple of 8).  The level's work list
 // is every pair's groups, pair-major; it is cut into 8 contiguous ranges, one per XCD (blocks are
 // dealt to the XCDs round-robin), each with its own queue head.  An XCD's waves thus work on
@@ -598,8 +509,9 @@ __global__ __launch_bounds__(64) void k_lk_A_rows(LkArgs a, const uint8_t* __res
 // separate launches from maxLevel down to 0; the position carried between them is next_pts (the
 // reference's nextPts[ptidx], stored every level).
 //
-// Rows arrive by LDS-DMA (buffer_load ... lds), one row ahead, retired by an explicit vmcnt(0)
-// at the top of the next row (the compiler does not track LDS-DMA):
+// Rows arrive by LDS-DMA (buffer_load ... lds), NB - 1 rows ahead, retired by an explicit vmcnt
+// at the top of each row (the compiler does not track LDS-DMA completion; it only orders LDS
+// reads after DMA into the same __shared__ object, hence one array per row buffer):
 //  * the union rows of all S slots: ND pieces of 1 KiB.  A piece's LDS destination is fixed
 //    (lane L writes bytes 16L..16L+15), so lane L of piece c loads the 16 B of whichever slot and
 //    pair offset that position holds in the [slot][UW][D, C] image -- source offsets are
@@ -952,10 +864,7 @@ static void launch_A(hipStream_t s, int batch, const LkArgs& a, const uint8_t* c
     constexpr int S = LkShape<G, UW>::S;
     const int ngroups = lk_groups<G, UW>(a, l);
     const dim3 grid((ngroups + S - 1) / S, batch);
-    if (l == a.maxl)   // the coarsest level runs before any iteration launch (see k_lk_A_rows)
-        hipLaunchKernelGGL((k_lk_A_rows<G, UW>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups);
-    else
-        hipLaunchKernelGGL((k_lk_A<G, UW>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups);
+    hipLaunchKernelGGL((k_lk_A<G, UW>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups);
 }
 
 template <int G, int UW>
