@@ -54,6 +54,16 @@ def main():
         busy = (e - s).sum() / (nw * span)
         print(f"level {L}: waves {nw}, span {span / 1e3:.0f} us, wave-time/(waves*span) {busy:.3f}, "
               f"after 10%/50%/90% exited: {q[0.1] / 1e3:.0f}/{q[0.5] / 1e3:.0f}/{q[0.9] / 1e3:.0f} us")
+        # per XCD (blocks are dealt round-robin: wave index & 7): first and last exit, and its
+        # waves' summed lifetime against waves x span -- imbalance between the XCDs' queue ranges
+        # shows as a spread of the last exits
+        idx = np.nonzero(ok)[0]
+        xs = []
+        for x in range(8):
+            sel = (idx & 7) == x
+            if sel.any():
+                xs.append(f"{x}:{e[sel].min() / 1e3:.0f}-{e[sel].max() / 1e3:.0f}")
+        print("    per-XCD first-last exit (us): " + " ".join(xs))
 
 
 if __name__ == "__main__":
