@@ -29,6 +29,8 @@ struct mdx_ctx {
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;               // LK class / A kernels run ahead here (MDX_LK_AUX=0: off)
     hipEvent_t lkev[kMaxLevels + 2] = {};    // launch_lk_v2's + the first frames' pyramids ready
+    hipStream_t iter2 = nullptr;             // LK dataflow: every other level's iteration launch (MDX_LK_FLOW)
+    hipEvent_t flowev[2] = {};
     mdx_params prm{};
     int max_w = 0, max_h = 0, max_batch = 0;
     DevBuf pyr1, pyr2, der, fits;            // pyramid / derivative / fit workspace
@@ -330,6 +332,11 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
         bool ok = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;
         for (int i = 0; ok && i <= kMaxLevels + 1; i++)
             ok = hipEventCreateWithFlags(&c->lkev[i], hipEventDisableTiming) == hipSuccess;
+        const char* ef = std::getenv("MDX_LK_FLOW");
+        if (ok && (!ef || std::atoi(ef) != 0)) {
+            ok = hipStreamCreateWithFlags(&c->iter2, hipStreamNonBlocking) == hipSuccess;
+            for (int i = 0; ok && i < 2; i++) ok = hipEventCreateWithFlags(&c->flowev[i], hipEventDisableTiming) == hipSuccess;
+        }
         if (!ok) {
             g_create_err = "aux stream / event creation failed";
             mdx_destroy(c);
@@ -363,7 +370,10 @@ extern "C" int mdx_destroy(mdx_ctx* c)
     }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->aux) (void)hipStreamDestroy(c->aux);
+    if (c->iter2) (void)hipStreamDestroy(c->iter2);
     for (hipEvent_t e : c->lkev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->flowev)
         if (e) (void)hipEventDestroy(e);
     delete c;
     return MDX_OK;
@@ -491,10 +501,13 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
         const char* e = std::getenv("MDX_LK_DEBUG_PT");
         a.dbg_pt = e ? std::atoi(e) : -1;
     }
+    // A sums, then the queue heads ([sub-batch][level][XCD]), then the dataflow counters ([level][pair])
     const size_t abytes = (size_t)g.nlev * batch * npts * sizeof(float4);
-    if ((rc = ensure(c, c->Abuf, abytes + (size_t)batch * kMaxLevels * 8 * sizeof(int))) != MDX_OK) return rc;
+    const size_t qbytes = (size_t)batch * kMaxLevels * 8 * sizeof(int);
+    if ((rc = ensure(c, c->Abuf, abytes + qbytes + (size_t)kMaxLevels * batch * sizeof(int))) != MDX_OK) return rc;
     HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
-                                  reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes), prev_ready));
+                                  reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes), prev_ready, c->iter2,
+                                  c->flowev, reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes + qbytes)));
     return MDX_OK;
 }
 

@@ -103,6 +103,10 @@ struct LkArgs {
                              // both grouped by residue class (ClassLevel::ord_off)
     const float* prev_pts;   // k_lk only: [batch][npts][2] start points (trajectories); null = the grid
     int max_sub;             // > 0: at most this many pairs per LK sub-batch (MDX_LK_SUB, tests)
+    int* done;               // LK v2 dataflow: [level][done_stride] groups retired per pair; null:
+                             // the level launches run one after another
+    int done_stride;
+    int dep_groups;          // > 0: groups per pair of the coarser level, which a group waits for
     float4* dbg;             // optional [batch][nlev][npts] (npx, npy, iters, status) at level end
     int dbg_pt;              // point whose per-iteration values are appended after dbg (pair 0)
 };
@@ -146,8 +150,13 @@ hipError_t launch_traj_update(hipStream_t s, int npts, const float* next_pts, co
 // + 1 events (no timing) used to order the two streams.  prev_ready (may be null): recorded by the
 // caller once the first frames' pyramids exist; the aux work waits on it instead of on everything
 // enqueued on s so far (the second frames' pyramids may still be in flight on s).
+// Dataflow (s2 and flow_ev[2] non-null, done: kMaxLevels x batch ints): the level launches alternate
+// between s and s2, so level L-1 starts in level L's tail; its groups wait for their pair's level-L
+// groups (done counters).  Used when every XCD's work range holds whole pairs (batch % 8 == 0) and
+// pairs' next_pts do not share 128-B lines (npts % 16 == 0).
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
-                        float4* Ab, int* qctr, hipEvent_t prev_ready = nullptr);
+                        float4* Ab, int* qctr, hipEvent_t prev_ready = nullptr, hipStream_t s2 = nullptr,
+                        hipEvent_t* flow_ev = nullptr, int* done = nullptr);
 // Grid rows [gy0, gy1) only (a row band; others are neither written nor counted).  cand != null:
 // row-band mode -- the band's count and first four accepted points go to *cand (one record per
 // pair) instead of a fit.

@@ -114,6 +114,10 @@ __device__ __forceinline__ void wave_lds_fence()
 #ifndef MDX_LK_NB
 #define MDX_LK_NB 2
 #endif
+// dataflow waits: at most this many s_sleep(8) polls (~0.1 s) before a group proceeds regardless
+// (and its wave stops waiting altogether): a wait that long means the hand-off failed, and the
+// results are then wrong rather than the launch hung
+constexpr int kLkSpinMax = 1 << 19;
 #ifndef MDX_LK_RFIRST
 #define MDX_LK_RFIRST 0
 #endif
@@ -575,7 +579,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
     uint32_t jrel = 0;                                            // pair's pyramid in jrs
     float A11 = 0.f, A12 = 0.f, A22 = 0.f, Dinv = 0.f;
     float nx = 0.f, ny = 0.f, npx = 0.f, npy = 0.f, pdx = 0.f, pdy = 0.f;
-    bool act = false;
+    bool act = false, gave_up = false;
     int status = 1, iters = 0;
 
     auto retire = [&]() {
@@ -586,8 +590,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
         if (q.valid && k == 0) {
             if (a.dbg)
                 a.dbg[((long long)pair * a.g.nlev + level) * a.npts + pt] = make_float4(npx, npy, (float)iters, (float)status);
-            reinterpret_cast<float2*>(a.next_pts)[po] = make_float2(npx, npy);
+            const float2 v = make_float2(npx, npy);
+            if (a.done)   // read by the next level's launch while this one runs: write-through (sc1)
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.next_pts) + po,
+                                   __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                reinterpret_cast<float2*>(a.next_pts)[po] = v;
             if (level == 0) a.status[po] = (uint8_t)status;
+        }
+        if (a.done && level > 0) {
+            // the group's points have their level result: once this wave's stores are done, one
+            // lane of the slot counts the group for its pair (MI355X_MICROARCH.md hand-off: sc1
+            // stores, vmcnt(0), agent atomic; the reader polls and loads sc1)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (sl == 0)
+                __hip_atomic_fetch_add(a.done + level * a.done_stride + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
 
@@ -621,7 +638,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                         npx = (float)(q.gx * a.pixel_step) * scale;
                         npy = (float)(q.gy * a.pixel_step) * scale;
                     } else {
-                        const float2 p = q.valid ? reinterpret_cast<const float2*>(a.next_pts)[po] : make_float2(0.f, 0.f);
+                        float2 p = make_float2(0.f, 0.f);
+                        if (a.dep_groups) {
+                            // dataflow: the coarser level may still run -- wait until every group of
+                            // this pair has retired there (bounded: its waves are resident and
+                            // drain their queue), then read the carried points past L1
+                            if (sl == 0 && !gave_up) {
+                                const int* d = a.done + (level + 1) * a.done_stride + pair;
+                                int t = 0;
+                                for (; t < kLkSpinMax; t++) {
+                                    if (__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.dep_groups) break;
+                                    __builtin_amdgcn_s_sleep(8);
+                                }
+                                if (t == kLkSpinMax) gave_up = true;
+                            }
+                            if (q.valid)
+                                p = __builtin_bit_cast(float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(a.next_pts) + po,
+                                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        } else if (q.valid) {
+                            p = reinterpret_cast<const float2*>(a.next_pts)[po];
+                        }
                         npx = p.x * 2.f;
                         npy = p.y * 2.f;
                     }
@@ -852,6 +888,17 @@ static int lk_iter_resident()
     return v;
 }
 
+// dataflow launches: percent of the resident waves each iteration launch takes (MDX_LK_CAP)
+static int lk_flow_cap()
+{
+    static const int cap = [] {
+        const char* e = std::getenv("MDX_LK_CAP");
+        const int v = e ? std::atoi(e) : 90;
+        return v < 10 ? 10 : v > 100 ? 100 : v;
+    }();
+    return cap;
+}
+
 template <int G, int UW>
 static int lk_groups(const LkArgs& a, int l)
 {
@@ -873,14 +920,19 @@ static void launch_iter(hipStream_t s, int batch, const LkArgs& a, const uint8_t
 {
     constexpr int S = LkShape<G, UW>::S;
     const int ngroups = lk_groups<G, UW>(a, l);
-    // persistent waves, a multiple of 8 so that every XCD range has waves
+    // persistent waves, a multiple of 8 so that every XCD range has waves.  Dataflow: each launch
+    // leaves part of the chip free, for the aux stream's class planes and A sums of the next level
+    // (which must be done before that level's launch can start) and for the coarser level's
+    // launch that this one may wait on
     const int need = (int)std::min<long long>(((long long)batch * ngroups + S - 1) / S, 1 << 30);
-    const int W = std::max(8, std::min((need + 7) / 8, lk_iter_resident<G, UW>() / 8) * 8);
+    int res = lk_iter_resident<G, UW>();
+    if (a.done) res = res * lk_flow_cap() / 100;
+    const int W = std::max(8, std::min((need + 7) / 8, res / 8) * 8);
     hipLaunchKernelGGL((k_lk_iter<G, UW>), dim3(W), dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups, batch);
 }
 
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
-                        float4* Ab, int* qctr, hipEvent_t prev_ready)
+                        float4* Ab, int* qctr, hipEvent_t prev_ready, hipStream_t s2, hipEvent_t* flow_ev, int* done)
 {
     // An XCD range spans at most ceil(n/8) + 1 pairs; its class slabs (and pyramids) must stay
     // addressable by 32-bit buffer offsets, so very large batches of large frames run in
@@ -945,18 +997,42 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
                 if (hipError_t e = hipEventRecord(ev[l], sa)) return e;
             }
         }
+        // dataflow: every XCD's work range must hold whole pairs (the hand-off stays in one L2) and
+        // no two pairs' carried points may share a 128-B line
+        const bool flow = aux && s2 && flow_ev && done && !b.dbg && nb % 8 == 0 && a.npts % 16 == 0 &&
+                          (reinterpret_cast<uintptr_t>(b.next_pts) & 127) == 0;
+        if (flow) {
+            if (hipError_t e = hipMemsetAsync(done, 0, sizeof(int) * kMaxLevels * nb, s)) return e;
+            if (hipError_t e = hipEventRecord(flow_ev[0], s)) return e;   // counters zeroed, front end done
+            if (hipError_t e = hipStreamWaitEvent(s2, flow_ev[0], 0)) return e;
+        }
         for (int l = a.maxl; l >= 0; l--) {
             const ClassLevel& C = a.plan.lv[l];
+            // levels alternate between the two streams: level l-1 is enqueued behind level l+1
+            // only, so it starts as level l's waves leave
+            hipStream_t st = flow && ((a.maxl - l) & 1) ? s2 : s;
             if (aux) {
-                if (hipError_t e = hipStreamWaitEvent(s, ev[l], 0)) return e;
+                if (hipError_t e = hipStreamWaitEvent(st, ev[l], 0)) return e;
+            }
+            LkArgs bl = b;
+            bl.done = flow ? done : nullptr;
+            bl.done_stride = nb;
+            bl.dep_groups = 0;
+            if (flow && l < a.maxl) {
+                const ClassLevel& Cp = a.plan.lv[l + 1];
+                bl.dep_groups = (Cp.nxp / Cp.G) * a.nyg;
             }
             const float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             switch (C.G * 1000 + C.UW) {
-#define LK_CASE(g, uw) case g * 1000 + uw: launch_iter<g, uw>(s, nb, b, bcls, bA, bq, l); break;
+#define LK_CASE(g, uw) case g * 1000 + uw: launch_iter<g, uw>(st, nb, bl, bcls, bA, bq, l); break;
                 LK_SHAPES
 #undef LK_CASE
             default: return hipErrorInvalidValue;
             }
+        }
+        if (flow) {   // join: everything after the LK (and the next sub-batch) follows both streams
+            if (hipError_t e = hipEventRecord(flow_ev[1], s2)) return e;
+            if (hipError_t e = hipStreamWaitEvent(s, flow_ev[1], 0)) return e;
         }
     }
     return hipGetLastError();

@@ -39,6 +39,15 @@ def main():
     st = buf[(n * nlev * B + STAMP_OFF) * 4:].reshape(K_MAX_LEVELS, WAVES, 4).astype(np.uint64)
     t0 = st[..., 0] | (st[..., 1] << np.uint64(32))
     t1 = st[..., 2] | (st[..., 3] << np.uint64(32))
+    # all levels together (with MDX_LK_FLOW the launches overlap): summed wave lifetimes against
+    # the resident capacity over the whole LK span
+    ok_all = t1[:nlev] > 0
+    s_all, e_all = t0[:nlev][ok_all].astype(np.int64), t1[:nlev][ok_all].astype(np.int64)
+    if len(s_all):
+        span_all = (e_all.max() - s_all.min()) * 10
+        cap = max(int(ok_all.sum(axis=1).max()), 1)
+        use = ((e_all - s_all) * 10).sum() / (cap * span_all)
+        print(f"all levels: span {span_all / 1e3:.0f} us, wave-time / (widest launch {cap} waves x span) {use:.3f}")
     for L in range(nlev - 1, -1, -1):
         ok = t1[L] > 0
         s, e = t0[L][ok].astype(np.int64), t1[L][ok].astype(np.int64)

@@ -152,19 +152,26 @@ def test_warp_diff_dev_batch(mdx, ctx, oracle):
         assert int((out[i] != ref).sum()) == 0, f"pair {i}"
 
 
-@pytest.mark.parametrize("B,env", [
-    (4, {}),
+@pytest.mark.parametrize("B,env,wh", [
+    (4, {}, (320, 240)),
     # 11 pairs: the LK queue's 8 per-XCD ranges split pairs; sub-batches of 3; both group sizes
-    (11, {"MDX_LK_SUB": "3"}),
-    (11, {"MDX_LK_G": "4"}),
-    (11, {"MDX_LK_G": "8"}),
-    (5, {"MDX_LK_AUX": "0"}),   # class / A kernels on the main stream
+    (11, {"MDX_LK_SUB": "3"}, (320, 240)),
+    (11, {"MDX_LK_G": "4"}, (320, 240)),
+    (11, {"MDX_LK_G": "8"}, (320, 240)),
+    (5, {"MDX_LK_AUX": "0"}, (320, 240)),   # class / A kernels on the main stream
+    # LK dataflow (batch a multiple of 8, npts a multiple of 16): level l-1's launch overlaps
+    # level l's and waits per pair; per sub-batch; off; group size 8 everywhere; a larger frame
+    (8, {}, (320, 240)),
+    (16, {"MDX_LK_SUB": "8"}, (320, 240)),
+    (8, {"MDX_LK_FLOW": "0"}, (320, 240)),
+    (8, {"MDX_LK_G": "8"}, (320, 240)),
+    (16, {}, (640, 480)),
 ])
-def test_batch_dev_matches_host_path(mdx, oracle, monkeypatch, B, env):
+def test_batch_dev_matches_host_path(mdx, oracle, monkeypatch, B, env, wh):
     """The zero-copy batched entry gives the same per-pair results as the oracle."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    w, h = 320, 240
+    w, h = wh
     pairs = [mdx.synth_pair(300 + i, w, h, 1) for i in range(B)]
     g1 = np.stack([p[0] for p in pairs]); g2 = np.stack([p[1] for p in pairs])
     n = mdx.grid_count(w, h, 10)
