@@ -160,8 +160,10 @@ int mdx_warp_diff_dev(mdx_ctx* ctx, int batch, const uint8_t* d_gray1, const uin
  *      smallest indices over all records; the fit, its inverse and num_vectors are then exactly
  *      the full path's.  Writes mask rows [y0, y1) to d_mask_band (row pitch w) and, when
  *      non-NULL, d_H[9] and d_num_vectors.
- * Both entries are asynchronous on the context stream and reuse the context's pyramids, so
- * step 3 must follow step 1 on the same context with no other call in between.  fit_mode must
+ * Both entries are asynchronous on the context stream.  Step 3 reads the pyramids of the
+ * context's latest mdx_band_flow_dev call, which must be of the same frame pair (several bands of
+ * one pair may run step 1 one after another first), and converts from that call's d_img1 the
+ * frame-1 rows its warp reads beyond the band, so d_img1 must still hold frame 1.  fit_mode must
  * be MDX_FIT_FIRST4.
  */
 typedef struct mdx_band_cand {

@@ -31,6 +31,21 @@ struct mdx_ctx {
     hipEvent_t lkev[kMaxLevels + 2] = {};    // launch_lk_v2's + the first frames' pyramids ready
     hipStream_t iter2 = nullptr;             // LK dataflow: every other level's iteration launch (MDX_LK_FLOW)
     hipEvent_t flowev[2] = {};
+    // Call pipelining (MDX_PIPE=1): the pyramid slabs have two halves used by alternate calls, and a
+    // call's front end runs on the aux stream right behind the previous call's last class planes
+    // and A sums, so it overlaps that call's last LK level and fit/warp.  (A stream of its own
+    // measured 1.9x slower: a process gets 4 hardware queues, and a fifth stream shares one, so
+    // its event waits block the work queued behind them.)
+    bool pipe = false;
+    hipEvent_t front_ev = nullptr;
+    hipEvent_t pyr_free[2] = {};             // on `stream`, after the last reader of each half
+    hipEvent_t lvl_done[kMaxLevels] = {};    // the last call's iteration launch of each level
+    int pyr_half = 0;                        // the half the next pipelined call writes
+    int last_half = 0;
+    uint8_t* last_pyr1 = nullptr;            // the last pair call's pyramids (band fit/warp, debug copies)
+    uint8_t* last_pyr2 = nullptr;
+    const uint8_t* band_img1 = nullptr;      // the last mdx_band_flow_dev's frame 1 (its fit/warp reads it)
+    int band_stride = 0, band_fmt = 0;
     mdx_params prm{};
     int max_w = 0, max_h = 0, max_batch = 0;
     DevBuf pyr1, pyr2, der, fits;            // pyramid / derivative / fit workspace
@@ -157,11 +172,15 @@ static int ensure(mdx_ctx* c, DevBuf& b, size_t need)
     return MDX_OK;
 }
 
+// Pyramid slabs hold two halves (call pipelining); non-pipelined users take the slab from its start.
+static size_t pyr_half_bytes(const DevBuf& b) { return b.cap / 2 / 256 * 256; }
+
 static int ensure_workspace(mdx_ctx* c, const Geometry& g, int batch)
 {
     int rc;
-    if ((rc = ensure(c, c->pyr1, (size_t)g.img_bytes * batch)) != MDX_OK) return rc;
-    if ((rc = ensure(c, c->pyr2, (size_t)g.img_bytes * batch)) != MDX_OK) return rc;
+    const size_t half = ((size_t)g.img_bytes * batch + 255) / 256 * 256;
+    if ((rc = ensure(c, c->pyr1, 2 * half)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->pyr2, 2 * half)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->der, (size_t)g.der_words * 4 * batch)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->fits, sizeof(PairFit) * (size_t)batch)) != MDX_OK) return rc;
     return MDX_OK;
@@ -337,6 +356,16 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
             ok = hipStreamCreateWithFlags(&c->iter2, hipStreamNonBlocking) == hipSuccess;
             for (int i = 0; ok && i < 2; i++) ok = hipEventCreateWithFlags(&c->flowev[i], hipEventDisableTiming) == hipSuccess;
         }
+        // opt-in: a pipelined device-entry call's front end does not wait for earlier work on the
+        // context stream, so its inputs must already be in HBM when the call is made
+        const char* ep = std::getenv("MDX_PIPE");
+        if (ok && ep && std::atoi(ep) != 0) {
+            c->pipe = true;
+            ok = hipEventCreateWithFlags(&c->front_ev, hipEventDisableTiming) == hipSuccess;
+            for (int i = 0; ok && i < 2; i++) ok = hipEventCreateWithFlags(&c->pyr_free[i], hipEventDisableTiming) == hipSuccess;
+            for (int i = 0; ok && i < kMaxLevels; i++)
+                ok = hipEventCreateWithFlags(&c->lvl_done[i], hipEventDisableTiming) == hipSuccess;
+        }
         if (!ok) {
             g_create_err = "aux stream / event creation failed";
             mdx_destroy(c);
@@ -371,6 +400,11 @@ extern "C" int mdx_destroy(mdx_ctx* c)
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->aux) (void)hipStreamDestroy(c->aux);
     if (c->iter2) (void)hipStreamDestroy(c->iter2);
+    if (c->front_ev) (void)hipEventDestroy(c->front_ev);
+    for (hipEvent_t e : c->pyr_free)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->lvl_done)
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->lkev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->flowev)
@@ -454,14 +488,22 @@ extern "C" int mdx_stage_ms(mdx_ctx* c, int stage, float* ms)
     return MDX_OK;
 }
 
-static inline void mark(mdx_ctx* c, int i)
+static inline void mark(mdx_ctx* c, int i, hipStream_t st = nullptr)
 {
     if (!c->timing || !c->ev) return;
     if (i == 0) {
         c->cur = c->ncalls < mdx_ctx::kSlots ? c->ncalls : -1;
         c->ncalls++;
     }
-    if (c->cur >= 0) (void)hipEventRecord(c->ev[c->cur * 7 + i], c->stream);
+    if (c->cur >= 0) (void)hipEventRecord(c->ev[c->cur * 7 + i], st ? st : c->stream);
+}
+
+// Non-pipelined users of the pyramid / derivative slabs (from the slab start, any size): the next
+// pipelined call's front end and aux work wait for them through both halves' events.
+static void release_pyr_all(mdx_ctx* c)
+{
+    for (hipEvent_t e : c->pyr_free)
+        if (e) (void)hipEventRecord(e, c->stream);
 }
 
 // The LK of a batch of pairs on the context's stream.  Grid start points (a.prev_pts null) on a
@@ -507,7 +549,8 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
     if ((rc = ensure(c, c->Abuf, abytes + qbytes + (size_t)kMaxLevels * batch * sizeof(int))) != MDX_OK) return rc;
     HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
                                   reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes), prev_ready, c->iter2,
-                                  c->flowev, reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes + qbytes)));
+                                  c->flowev, reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes + qbytes),
+                                  c->pipe ? c->lvl_done : nullptr));
     return MDX_OK;
 }
 
@@ -539,7 +582,7 @@ static void band_rows(const Geometry& g, const ClassPlan& P, RowSpan* rows)
 static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint8_t* d_img2, int w, int h, int stride,
                         size_t frame_stride, int fmt, float* d_np, uint8_t* d_st, double* d_vec, uint8_t* d_mask,
                         double* d_H, const double* d_Hext, int* d_num, int gy0 = 0, int gy1 = -1,
-                        mdx_band_cand* cand = nullptr)
+                        mdx_band_cand* cand = nullptr, bool may_overlap = false)
 {
     const mdx_params& P = c->prm;
     if (w <= 0 || h <= 0 || batch <= 0) return set_err(c, MDX_EINVAL, "bad frame size or batch");
@@ -561,8 +604,24 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
     uint8_t* pyr2 = c->pyr2.as<uint8_t>();
     uint32_t* der = c->der.as<uint32_t>();
     PairFit* fits = c->fits.as<PairFit>();
+    // call pipelining: this call's pyramids go to the half the previous call did not use, and its
+    // front end runs on the front stream once that half's last reader (two calls back) is done
+    const bool pipe = may_overlap && c->pipe && c->aux && c->lk_impl == 2;
+    hipStream_t fs_ = s;
+    int half = 0;
+    if (pipe) {
+        half = c->pyr_half;
+        c->pyr_half ^= 1;
+        pyr1 += half * pyr_half_bytes(c->pyr1);
+        pyr2 += half * pyr_half_bytes(c->pyr2);
+        fs_ = c->aux;
+        HIP_OR_RETURN(c, hipStreamWaitEvent(fs_, c->pyr_free[half], 0));
+    }
+    c->last_pyr1 = pyr1;
+    c->last_pyr2 = pyr2;
+    c->last_half = half;
 
-    mark(c, 0);
+    mark(c, 0, fs_);
     // The class planes and A sums need only the first frames' pyramids: build those first and let
     // the aux stream start on them while the second frames' pyramids are built.  Stage "gray_pad"
     // = gray + pad + level 1 of the first frames (k_front), "pyrdown" = the rest of the pyramids.
@@ -579,19 +638,24 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         }
     }
     if (c->aux && c->lk_impl == 2) {
-        HIP_OR_RETURN(c, launch_front(s, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g, 1, prows));
-        mark(c, 1);
-        HIP_OR_RETURN(c, launch_pyr_levels(s, batch, pyr1, pyr2, g, 1, prows));
-        HIP_OR_RETURN(c, hipEventRecord(c->lkev[kMaxLevels + 1], s));
+        HIP_OR_RETURN(c, launch_front(fs_, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g, 1, prows));
+        mark(c, 1, fs_);
+        HIP_OR_RETURN(c, launch_pyr_levels(fs_, batch, pyr1, pyr2, g, 1, prows));
+        HIP_OR_RETURN(c, hipEventRecord(c->lkev[kMaxLevels + 1], fs_));
         prev_ready = c->lkev[kMaxLevels + 1];
-        HIP_OR_RETURN(c, launch_front(s, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g, 2));
-        HIP_OR_RETURN(c, launch_pyr_levels(s, batch, pyr1, pyr2, g, 2));
+        HIP_OR_RETURN(c, launch_front(fs_, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g, 2));
+        HIP_OR_RETURN(c, launch_pyr_levels(fs_, batch, pyr1, pyr2, g, 2));
+        if (pipe) {
+            mark(c, 2, fs_);
+            HIP_OR_RETURN(c, hipEventRecord(c->front_ev, fs_));
+            HIP_OR_RETURN(c, hipStreamWaitEvent(s, c->front_ev, 0));
+        }
     } else {
         HIP_OR_RETURN(c, launch_front(s, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g));
         mark(c, 1);
         HIP_OR_RETURN(c, launch_pyr_levels(s, batch, pyr1, pyr2, g));
     }
-    mark(c, 2);
+    if (!pipe) mark(c, 2);
     // Scharr derivatives feed only the LK.  The class-plane LK launches them itself, on its
     // aux stream right before each level's class planes, so they overlap the coarser levels'
     // iterations; the single-kernel LK needs them up front.
@@ -621,6 +685,10 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
                                          fits, P.fit_mode, d_Hext, c->csum.p, cand));
     mark(c, 5);
     if (cand) {
+        // mdx_band_fit_warp_dev reads the latest band call's pyramids (same frame pair), whichever
+        // half they are in, and records their release again after its warp
+        if (pipe) HIP_OR_RETURN(c, hipEventRecord(c->pyr_free[half], s));
+        else release_pyr_all(c);
         mark(c, 6);
         return MDX_OK;
     }
@@ -632,6 +700,8 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
                                           d_mask, (long long)w * h, P.thresh));
     }
     if (d_H || d_num) HIP_OR_RETURN(c, launch_export_fit(s, batch, fits, d_H, d_num));
+    if (pipe) HIP_OR_RETURN(c, hipEventRecord(c->pyr_free[half], s));
+    else release_pyr_all(c);
     mark(c, 6);
     return MDX_OK;
 }
@@ -655,7 +725,7 @@ extern "C" int mdx_flow_warp_diff_batch_dev(mdx_ctx* c, int batch, const uint8_t
         d_status = c->bst.as<uint8_t>();
     }
     return run_pipeline(c, batch, d_img1, d_img2, w, h, stride, frame_stride, fmt, d_next_pts, d_status, d_vectors,
-                        d_mask, d_H, d_H_external, d_num_vectors);
+                        d_mask, d_H, d_H_external, d_num_vectors, 0, -1, nullptr, true);
 }
 
 extern "C" int mdx_flow_warp_diff(mdx_ctx* c, const uint8_t* img1, const uint8_t* img2, int w, int h, int stride,
@@ -819,7 +889,9 @@ extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int n
     }
     fp[npairs] = pyr2 + (size_t)g.img_bytes * (npairs - 1);
     fd[npairs] = nullptr;
-    return trajectory_passes(c, g, nimg, w, h, fp.data(), fd.data(), traj, traj_len, start_pts, vectors, num_vectors);
+    rc = trajectory_passes(c, g, nimg, w, h, fp.data(), fd.data(), traj, traj_len, start_pts, vectors, num_vectors);
+    release_pyr_all(c);
+    return rc;
 }
 
 // The resident ring (include/mdx.h): slot k of ring_pyr / ring_der holds one frame's padded pyramid
@@ -1050,10 +1122,13 @@ extern "C" int mdx_band_flow_dev(mdx_ctx* c, const uint8_t* d_img1, const uint8_
     const int gy0 = (y0 + ps - 1) / ps, gy1 = (y1 + ps - 1) / ps;
     c->band_w = c->band_h = 0;
     const int rc = run_pipeline(c, 1, d_img1, d_img2, w, h, stride, (size_t)stride * h, fmt, d_next_pts, d_status,
-                                d_vectors, nullptr, nullptr, nullptr, nullptr, gy0, gy1, d_cand);
+                                d_vectors, nullptr, nullptr, nullptr, nullptr, gy0, gy1, d_cand, true);
     if (rc == MDX_OK) {
         c->band_w = w;
         c->band_h = h;
+        c->band_img1 = d_img1;
+        c->band_stride = stride;
+        c->band_fmt = fmt;
     }
     return rc;
 }
@@ -1070,13 +1145,21 @@ extern "C" int mdx_band_fit_warp_dev(mdx_ctx* c, int nrec, const mdx_band_cand* 
     const Geometry g = make_geometry(w, h, c->prm.max_level);
     hipStream_t s = c->stream;
     PairFit* fits = c->fits.as<PairFit>();
-    HIP_OR_RETURN(c, launch_band_fit(s, nrec, d_cands, fits));
+    if (!c->last_pyr1 || !c->band_img1) return set_err(c, MDX_EINVAL, "mdx_band_fit_warp_dev: no mdx_band_flow_dev before");
+    HIP_OR_RETURN(c, launch_band_fit(s, nrec, d_cands, fits, w, h, y0, y1));
     const Level& L0 = g.lv[0];
-    const uint8_t* g1 = c->pyr1.as<uint8_t>() + L0.img_off + L0.core();
-    const uint8_t* g2 = c->pyr2.as<uint8_t>() + L0.img_off + L0.core();
+    // the band's flow built frame 1's pyramid for its own rows only: the rows this band's warp
+    // reads beyond them (the fit is known now) are converted from the frame
+    HIP_OR_RETURN(c, launch_gray_rows(s, c->band_img1, w, h, c->band_stride, c->band_fmt,
+                                      c->last_pyr1 + L0.img_off + L0.core(), L0.pitch, fits));
+    const uint8_t* g1 = c->last_pyr1 + L0.img_off + L0.core();
+    const uint8_t* g2 = c->last_pyr2 + L0.img_off + L0.core();
     HIP_OR_RETURN(c, launch_warp_diff(s, 1, g1, g.img_bytes, L0.pitch, g2, g.img_bytes, L0.pitch, w, h, fits, d_mask_band,
                                       (long long)w * (y1 - y0), c->prm.thresh, y0, y1));
     if (d_H || d_num_vectors) HIP_OR_RETURN(c, launch_export_fit(s, 1, fits, d_H, d_num_vectors));
+    // the band's pyramids have been read: the pipelined call two calls on may overwrite them
+    if (c->pipe) HIP_OR_RETURN(c, hipEventRecord(c->pyr_free[c->last_half], s));
+    else release_pyr_all(c);
     return MDX_OK;
 }
 
@@ -1088,7 +1171,12 @@ extern "C" int mdx_debug_copy(mdx_ctx* c, int which, void* dst, size_t bytes)
               : which == 4 ? c->der : c->cls;
     if (!b.p) return set_err(c, MDX_EINVAL, "debug buffer %d unavailable", which);
     HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
-    HIP_OR_RETURN(c, hipMemcpy(dst, b.p, bytes < b.cap ? bytes : b.cap, hipMemcpyDeviceToHost));
+    // pyramids: the half the last pair call wrote
+    const uint8_t* src = static_cast<const uint8_t*>(b.p);
+    if (which == 2 && c->last_pyr1) src = c->last_pyr1;
+    if (which == 3 && c->last_pyr2) src = c->last_pyr2;
+    const size_t avail = b.cap - (size_t)(src - static_cast<const uint8_t*>(b.p));
+    HIP_OR_RETURN(c, hipMemcpy(dst, src, bytes < avail ? bytes : avail, hipMemcpyDeviceToHost));
     return MDX_OK;
 }
 

@@ -44,7 +44,7 @@ struct PairFit {
     double Hinv[9];   // matrix warpPerspective actually samples with (inverse or all-zero)
     int num_vectors;  // accepted vectors (reference return value)
     int fit_status;   // 0 fitted, 1 no vectors, 2 fewer than 4 vectors
-    int pad_[2];
+    int src_y0, src_y1;   // row bands (k_band_fit): frame-1 rows the band's warp reads
 };
 
 // Residue-class planes of LK v2 (mdx_lk.hip): per level, one plane set per class of
@@ -154,9 +154,12 @@ hipError_t launch_traj_update(hipStream_t s, int npts, const float* next_pts, co
 // between s and s2, so level L-1 starts in level L's tail; its groups wait for their pair's level-L
 // groups (done counters).  Used when every XCD's work range holds whole pairs (batch % 8 == 0) and
 // pairs' next_pts do not share 128-B lines (npts % 16 == 0).
+// lvl_done (may be null: calls do not overlap): [kMaxLevels] events, re-recorded after each level's
+// iteration launch; the aux stream waits for the previous call's before rewriting that level's
+// class planes, A sums and queue heads (call pipelining lets the aux stream run a call ahead).
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
                         float4* Ab, int* qctr, hipEvent_t prev_ready = nullptr, hipStream_t s2 = nullptr,
-                        hipEvent_t* flow_ev = nullptr, int* done = nullptr);
+                        hipEvent_t* flow_ev = nullptr, int* done = nullptr, hipEvent_t* lvl_done = nullptr);
 // Grid rows [gy0, gy1) only (a row band; others are neither written nor counted).  cand != null:
 // row-band mode -- the band's count and first four accepted points go to *cand (one record per
 // pair) instead of a fit.
@@ -165,9 +168,14 @@ hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, 
                                PairFit* fits, int fit_mode, const double* H_external, void* scratch,
                                mdx_band_cand* cand);
 // Merge nrec band records (first four accepted overall = four smallest indices) and fit
-hipError_t launch_band_fit(hipStream_t s, int nrec, const mdx_band_cand* cands, PairFit* fit);
+hipError_t launch_band_fit(hipStream_t s, int nrec, const mdx_band_cand* cands, PairFit* fit, int w, int h, int y0,
+                           int y1);
 // bytes of the scratch launch_classify_fit needs
 inline size_t classify_scratch_bytes(int batch, int npts) { return (size_t)batch * ((npts + 255) / 256) * 32; }
+// Row bands: frame-1 gray rows [fit->src_y0, fit->src_y1) into the padded level 0 of pyr1 (the
+// band's warp may read rows its own pyramid build skipped).  gray1_l0: level-0 core, pitch bytes.
+hipError_t launch_gray_rows(hipStream_t s, const uint8_t* img1, int w, int h, int stride, int fmt, uint8_t* gray1_l0,
+                            int pitch, const PairFit* fit);
 hipError_t launch_set_fit_external(hipStream_t s, int batch, const double* H_external, PairFit* fits);
 // Destination rows [row0, row1) of every pair (row1 <= h); mask row y is at mask + (y - row0) * w.
 hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,

@@ -1065,7 +1065,44 @@ __global__ __launch_bounds__(64) void k_band_record(const float* __restrict__ ne
 // Merge the bands' records: the four smallest indices over all records are the frame's first four
 // accepted points (each band lists its own first four, and bands partition the points), so the
 // fit below is bit-identical to the full path's k_fit.
-__global__ void k_band_fit(const mdx_band_cand* __restrict__ cands, int nrec, PairFit* __restrict__ fit)
+// Frame-1 rows the warp of destination rows [y0, y1) reads: under M (= Hinv) a rectangle whose
+// corners all have W of one sign maps to the convex quadrilateral of the corners' images, so
+// their Y bound the source rows (+-2 for the reference's 1/32-px rounding and the lower tap);
+// otherwise every row.  M all zero (singular fit): the constant warp reads row 0 (and 1).
+__device__ void band_source_rows(const double* M, int w, int h, int y0, int y1, int& r0, int& r1)
+{
+    bool zero = true;
+    for (int k = 0; k < 9; k++) zero = zero && M[k] == 0.0;
+    r0 = 0;
+    r1 = h;
+    if (zero) {
+        r1 = min(h, 2);
+        return;
+    }
+    double ymin = 0.0, ymax = 0.0;
+    int sgn = 0;
+    for (int q = 0; q < 4; q++) {
+        const double x = (q & 1) ? (double)(w - 1) : 0.0, y = (q & 2) ? (double)(y1 - 1) : (double)y0;
+        const double W = M[6] * x + M[7] * y + M[8];
+        const int sq = W > 0.0 ? 1 : W < 0.0 ? -1 : 0;
+        if (sq == 0 || (q && sq != sgn)) return;
+        sgn = sq;
+        const double Y = (M[3] * x + M[4] * y + M[5]) / W;
+        if (!(Y == Y) || __builtin_isinf(Y)) return;
+        ymin = q ? fmin(ymin, Y) : Y;
+        ymax = q ? fmax(ymax, Y) : Y;
+    }
+    if (ymax < -4.0 || ymin > (double)h + 4.0) {   // footprint outside the frame: nothing to read
+        r0 = r1 = 0;
+        return;
+    }
+    r0 = (int)fmax(0.0, floor(ymin) - 2.0);
+    r1 = (int)fmin((double)h, floor(ymax) + 3.0);
+    if (r1 < r0) r1 = r0;
+}
+
+__global__ void k_band_fit(const mdx_band_cand* __restrict__ cands, int nrec, PairFit* __restrict__ fit, int w, int h,
+                           int y0, int y1)
 {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     int total = 0;
@@ -1094,10 +1131,43 @@ __global__ void k_band_fit(const mdx_band_cand* __restrict__ cands, int nrec, Pa
         dev_perspective_fit(bs, bd, f.H, fw);
         dev_invert3x3(f.H, f.Hinv);
         f.fit_status = 0;
+        band_source_rows(f.Hinv, w, h, y0, y1, f.src_y0, f.src_y1);
     } else {
         for (int k = 0; k < 9; k++) { f.H[k] = 0.0; f.Hinv[k] = 0.0; }
         f.fit_status = total == 0 ? 1 : 2;
+        f.src_y0 = f.src_y1 = 0;   // no warp (zero mask)
     }
+}
+
+// Rows [fit->src_y0, fit->src_y1) of frame 1 -> gray, into the padded level-0 core (what k_front
+// writes there): block (bx, by) converts 256 columns of rows src_y0 + by, + gridDim.y, ...
+__global__ __launch_bounds__(64) void k_gray_rows(const uint8_t* __restrict__ img1, int w, int stride, int fmt,
+                                                  uint8_t* __restrict__ g, int pitch, const PairFit* __restrict__ fit)
+{
+    const int r0 = fit->src_y0, r1 = fit->src_y1;
+    const int x = (blockIdx.x * 64 + threadIdx.x) * 4;
+    if (x >= w) return;
+    for (int y = r0 + (int)blockIdx.y; y < r1; y += gridDim.y) {
+        const uint8_t* sp = img1 + (long long)y * stride;
+        uint8_t* dp = g + (long long)y * pitch + x;
+        const int n = min(4, w - x);
+        uint32_t d = 0;
+        for (int i = 0; i < n; i++) {
+            const int v = fmt == 0 ? sp[x + i] : gray_of(sp + 3 * (x + i), fmt);
+            d |= (uint32_t)v << (8 * i);
+        }
+        if (n == 4) *reinterpret_cast<uint32_t*>(dp) = d;   // x and the core are 4-B aligned
+        else for (int i = 0; i < n; i++) dp[i] = (uint8_t)(d >> (8 * i));
+    }
+}
+
+hipError_t launch_gray_rows(hipStream_t s, const uint8_t* img1, int w, int h, int stride, int fmt, uint8_t* gray1_l0,
+                            int pitch, const PairFit* fit)
+{
+    (void)h;
+    const dim3 grid((w + 255) / 256, 64);
+    hipLaunchKernelGGL(k_gray_rows, grid, dim3(64), 0, s, img1, w, stride, fmt, gray1_l0, pitch, fit);
+    return hipGetLastError();
 }
 
 __global__ void k_set_fit_external(const double* __restrict__ H_ext, PairFit* __restrict__ fits, int batch)
@@ -1336,9 +1406,10 @@ hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, 
     return hipGetLastError();
 }
 
-hipError_t launch_band_fit(hipStream_t s, int nrec, const mdx_band_cand* cands, PairFit* fit)
+hipError_t launch_band_fit(hipStream_t s, int nrec, const mdx_band_cand* cands, PairFit* fit, int w, int h, int y0,
+                           int y1)
 {
-    hipLaunchKernelGGL(k_band_fit, dim3(1), dim3(64), 0, s, cands, nrec, fit);
+    hipLaunchKernelGGL(k_band_fit, dim3(1), dim3(64), 0, s, cands, nrec, fit, w, h, y0, y1);
     return hipGetLastError();
 }
 

@@ -893,7 +893,7 @@ static int lk_flow_cap()
 {
     static const int cap = [] {
         const char* e = std::getenv("MDX_LK_CAP");
-        const int v = e ? std::atoi(e) : 90;
+        const int v = e ? std::atoi(e) : 80;
         return v < 10 ? 10 : v > 100 ? 100 : v;
     }();
     return cap;
@@ -932,7 +932,8 @@ static void launch_iter(hipStream_t s, int batch, const LkArgs& a, const uint8_t
 }
 
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
-                        float4* Ab, int* qctr, hipEvent_t prev_ready, hipStream_t s2, hipEvent_t* flow_ev, int* done)
+                        float4* Ab, int* qctr, hipEvent_t prev_ready, hipStream_t s2, hipEvent_t* flow_ev, int* done,
+                        hipEvent_t* lvl_done)
 {
     // An XCD range spans at most ceil(n/8) + 1 pairs; its class slabs (and pyramids) must stay
     // addressable by 32-bit buffer offsets, so very large batches of large frames run in
@@ -967,6 +968,9 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         }
         for (int l = a.maxl; l >= 0; l--) {
             const ClassLevel& C = a.plan.lv[l];
+            if (aux && lvl_done) {   // the previous call's level-l iterations read these planes / sums
+                if (hipError_t e = hipStreamWaitEvent(sa, lvl_done[l], 0)) return e;
+            }
             LkClassArgs ca;
             ca.g = a.g;
             ca.plan = a.plan;
@@ -1028,6 +1032,9 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
                 LK_SHAPES
 #undef LK_CASE
             default: return hipErrorInvalidValue;
+            }
+            if (lvl_done) {
+                if (hipError_t e = hipEventRecord(lvl_done[l], st)) return e;
             }
         }
         if (flow) {   // join: everything after the LK (and the next sub-batch) follows both streams

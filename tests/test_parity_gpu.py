@@ -300,3 +300,100 @@ def test_full_path_8k_rgb_bit_exact(mdx, oracle):
         res = c.flow_warp_diff(a, b, fmt=mdx.FMT_RGB8)
     ref = oracle.calculate_optical_flow(a, b, fmt=oracle.FMT_RGB8, nthreads=16, pixel_step=10, min_vector_size=1.0)
     _compare(res, ref, "8k rgb")
+
+
+@pytest.mark.parametrize("env", [{"MDX_PIPE": "1"}, {}])
+def test_back_to_back_calls_pipelined(mdx, oracle, monkeypatch, env):
+    """Calls enqueued back to back without a host sync (the bench's pattern): with call pipelining
+    (MDX_PIPE=1, inputs resident before each call) each call's front end runs beside the previous
+    call's last level and fit/warp, on the other half of the pyramid slabs.  Four calls on three different batches into separate outputs, a
+    synchronous trajectory call in between: every call's results equal the oracle's."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    w, h, B = 320, 240, 8
+    n = mdx.grid_count(w, h, 10)
+    sets = [[mdx.synth_pair(700 + 10 * s + i, w, h, 1) for i in range(B)] for s in range(3)]
+    order = [0, 1, 2, 0]
+    with mdx.Context(0, w, h, B) as c:
+        c.set_params(pixel_step=10)
+        ins = []
+        for pairs in sets:
+            g1 = np.stack([p[0] for p in pairs]); g2 = np.stack([p[1] for p in pairs])
+            d1, d2 = c.dev_alloc(g1.nbytes), c.dev_alloc(g2.nbytes)
+            c.h2d(d1, g1); c.h2d(d2, g2)
+            ins.append((d1, d2))
+        outs = [{k: c.dev_alloc(s) for k, s in dict(np=B * n * 8, st=B * n, mask=B * w * h, num=B * 4).items()}
+                for _ in order]
+        for j, si in enumerate(order):
+            d1, d2 = ins[si]
+            o = outs[j]
+            c.flow_warp_diff_batch_dev(B, d1, d2, w, h, w, w * h, mdx.FMT_GRAY8, o["np"], o["st"], 0, o["mask"], 0, 0,
+                                       o["num"])
+            if j == 1:   # a synchronous entry on the shared slabs between pipelined calls
+                seq = [sets[2][0][0], sets[2][0][1], sets[2][1][0]]
+                tr = c.flow_trajectory(seq)
+                ref_tr = oracle.flow_trajectory(seq, pixel_step=10)
+                assert tr.num_vectors == ref_tr["num_vectors"]
+        c.sync()
+        got = []
+        for o in outs:
+            r = dict(np=np.empty((B, n, 2), np.float32), st=np.empty((B, n), np.uint8),
+                     mask=np.empty((B, h, w), np.uint8), num=np.empty(B, np.int32))
+            for k, arr in r.items():
+                c.d2h(arr, o[k])
+            got.append(r)
+        for o in outs:
+            for p in o.values():
+                c.dev_free(p)
+        for d1, d2 in ins:
+            c.dev_free(d1); c.dev_free(d2)
+    for j, si in enumerate(order):
+        for i in range(B):
+            ref = oracle.calculate_optical_flow(sets[si][i][0], sets[si][i][1], pixel_step=10)
+            assert got[j]["num"][i] == ref["num_vectors"], (j, i)
+            np.testing.assert_array_equal(got[j]["st"][i], ref["status"])
+            np.testing.assert_array_equal(got[j]["np"][i].view(np.uint32), ref["next_pts"].view(np.uint32))
+            np.testing.assert_array_equal(got[j]["mask"][i], ref["mask"])
+
+
+@pytest.mark.parametrize("w,h,ps,nb,ch", [(640, 480, 10, 4, 1), (1280, 720, 7, 3, 3)])
+def test_row_bands_on_separate_contexts(mdx, w, h, ps, nb, ch):
+    """Each band on its own context, as on its own GPU: a band's flow builds frame 1's pyramid for
+    its rows only, so the rows its warp reads beyond the band (camera motion) come from the frame
+    at fit/warp time.  Every mask row equals the full path's."""
+    from motion_detection_amd import rowtile
+    a, b, _ = mdx.synth_pair(7100 + nb, w, h, ch)
+    fmt = mdx.FMT_GRAY8 if ch == 1 else mdx.FMT_RGB8
+    n = mdx.grid_count(w, h, ps)
+    ctxs = [mdx.Context(0, w, h, 1, pixel_step=ps, min_vector_size=1.0) for _ in range(nb)]
+    try:
+        full = ctxs[0].flow_warp_diff(a, b, fmt=fmt)
+        recs = np.empty(nb, rowtile.BAND_CAND_DTYPE)
+        bufs = []
+        for r, c in enumerate(ctxs):
+            d = {k: c.dev_alloc(sz) for k, sz in dict(i1=a.nbytes, i2=b.nbytes, np=n * 8, st=n, cand=96,
+                                                       cands=nb * 96, mask=w * h, num=4).items()}
+            c.h2d(d["i1"], a); c.h2d(d["i2"], b)
+            y0, y1 = rowtile.band_rows(h, nb, r)
+            c.band_flow_dev(d["i1"], d["i2"], w, h, w * ch, fmt, y0, y1, d["np"], d["st"], d["cand"])
+            c.sync()
+            one = np.empty(1, rowtile.BAND_CAND_DTYPE)
+            c.d2h(one, d["cand"])
+            recs[r] = one[0]
+            bufs.append(d)
+        mask = np.empty((h, w), np.uint8)
+        for r, (c, d) in enumerate(zip(ctxs, bufs)):
+            y0, y1 = rowtile.band_rows(h, nb, r)
+            c.h2d(d["cands"], recs.view(np.uint8))
+            c.band_fit_warp_dev(nb, d["cands"], y0, y1, d["mask"], 0, d["num"])
+            c.sync()
+            band = np.empty((y1 - y0, w), np.uint8)
+            c.d2h(band, d["mask"])
+            mask[y0:y1] = band
+        for c, d in zip(ctxs, bufs):
+            for p in d.values():
+                c.dev_free(p)
+    finally:
+        for c in ctxs:
+            c.close()
+    assert int((mask != full.mask).sum()) == 0
