@@ -868,6 +868,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
     }
 }
 
+// Dataflow gate: one wave, launched on the next level's stream right before that level's
+// iteration launch, returns once every XCD's queue of `level` (T groups in 8 ranges) has been
+// handed out -- the start of that level's tail.  The next level's persistent waves are then
+// dispatched only into the slots the tail frees; launched while the level still had its whole
+// queue ahead, they took half the chip and spun there (both launches ~2x slower, measured).
+// Bounded like the group waits (~0.1 s).
+__global__ __launch_bounds__(64) void k_lk_gate(const int* __restrict__ qctr, long long T)
+{
+    const int x = threadIdx.x;
+    if (x >= 8) return;
+    const long long cb = T * x / 8, ce = T * (x + 1) / 8;
+    for (int t = 0; t < kLkSpinMax; t++) {
+        if (__hip_atomic_load(qctr + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ce - cb) break;
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
 // persistent waves for k_lk_iter: what the current device keeps resident at once (cached per
 // device; contexts on several devices may launch from several host threads)
 template <int G, int UW>
@@ -1025,6 +1042,9 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             if (flow && l < a.maxl) {
                 const ClassLevel& Cp = a.plan.lv[l + 1];
                 bl.dep_groups = (Cp.nxp / Cp.G) * a.nyg;
+            }
+            if (bl.dep_groups) {   // start in the coarser level's tail, not beside its whole queue
+                hipLaunchKernelGGL(k_lk_gate, dim3(1), dim3(64), 0, st, bq + (l + 1) * 8, (long long)nb * bl.dep_groups);
             }
             const float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             switch (C.G * 1000 + C.UW) {
