@@ -910,7 +910,7 @@ static int lk_flow_cap()
 {
     static const int cap = [] {
         const char* e = std::getenv("MDX_LK_CAP");
-        const int v = e ? std::atoi(e) : 80;
+        const int v = e ? std::atoi(e) : 85;
         return v < 10 ? 10 : v > 100 ? 100 : v;
     }();
     return cap;
