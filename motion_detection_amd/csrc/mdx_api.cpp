@@ -45,6 +45,7 @@ struct mdx_ctx {
     uint8_t* last_pyr1 = nullptr;            // the last pair call's pyramids (band fit/warp, debug copies)
     uint8_t* last_pyr2 = nullptr;
     const uint8_t* band_img1 = nullptr;      // the last mdx_band_flow_dev's frame 1 (its fit/warp reads it)
+    int band_built[2] = {0, 0};              // level-0 rows of frame 1 that call's pyramid build wrote
     int band_stride = 0, band_fmt = 0;
     mdx_params prm{};
     int max_w = 0, max_h = 0, max_batch = 0;
@@ -545,8 +546,9 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
     }
     // A sums, then the queue heads ([sub-batch][level][XCD]), then the dataflow counters ([level][pair])
     const size_t abytes = (size_t)g.nlev * batch * npts * sizeof(float4);
-    const size_t qbytes = (size_t)batch * kMaxLevels * 8 * sizeof(int);
-    if ((rc = ensure(c, c->Abuf, abytes + qbytes + (size_t)kMaxLevels * batch * sizeof(int))) != MDX_OK) return rc;
+    const size_t qbytes = (size_t)batch * kMaxLevels * 8 * kCtrPad * sizeof(int);
+    if ((rc = ensure(c, c->Abuf, abytes + qbytes + (size_t)kMaxLevels * batch * kCtrPad * sizeof(int))) != MDX_OK)
+        return rc;
     HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
                                   reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes), prev_ready, c->iter2,
                                   c->flowev, reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes + qbytes),
@@ -636,6 +638,15 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
             band_rows(g, c->plan, rows);
             prows = rows;
         }
+    }
+    // level-0 rows of frame 1 this call builds (mdx_band_fit_warp_dev converts the others it needs);
+    // k_front writes whole level-1 bands, i.e. level-0 rows 2*lo1 .. 2*hi1 of the widened range
+    c->band_built[0] = 0;
+    c->band_built[1] = h;
+    if (prows) {
+        const int lo1 = std::min(rows[1].lo, rows[0].lo / 2), hi1 = std::max(rows[1].hi, (rows[0].hi + 1) / 2);
+        c->band_built[0] = std::max(0, 2 * lo1);
+        c->band_built[1] = std::min(h, 2 * hi1);
     }
     if (c->aux && c->lk_impl == 2) {
         HIP_OR_RETURN(c, launch_front(fs_, batch, d_img1, d_img2, w, h, stride, fs, fmt, pyr1, pyr2, g, 1, prows));
@@ -1151,7 +1162,8 @@ extern "C" int mdx_band_fit_warp_dev(mdx_ctx* c, int nrec, const mdx_band_cand* 
     // the band's flow built frame 1's pyramid for its own rows only: the rows this band's warp
     // reads beyond them (the fit is known now) are converted from the frame
     HIP_OR_RETURN(c, launch_gray_rows(s, c->band_img1, w, h, c->band_stride, c->band_fmt,
-                                      c->last_pyr1 + L0.img_off + L0.core(), L0.pitch, fits));
+                                      c->last_pyr1 + L0.img_off + L0.core(), L0.pitch, fits, c->band_built[0],
+                                      c->band_built[1]));
     const uint8_t* g1 = c->last_pyr1 + L0.img_off + L0.core();
     const uint8_t* g2 = c->last_pyr2 + L0.img_off + L0.core();
     HIP_OR_RETURN(c, launch_warp_diff(s, 1, g1, g.img_bytes, L0.pitch, g2, g.img_bytes, L0.pitch, w, h, fits, d_mask_band,

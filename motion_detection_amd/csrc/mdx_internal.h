@@ -103,13 +103,20 @@ struct LkArgs {
                              // both grouped by residue class (ClassLevel::ord_off)
     const float* prev_pts;   // k_lk only: [batch][npts][2] start points (trajectories); null = the grid
     int max_sub;             // > 0: at most this many pairs per LK sub-batch (MDX_LK_SUB, tests)
-    int* done;               // LK v2 dataflow: [level][done_stride] groups retired per pair; null:
+    int* done;               // LK v2 dataflow: [level][done_stride] groups retired per pair, each
+                             // counter on its own 128-B line (kCtrPad ints); null:
                              // the level launches run one after another
     int done_stride;
     int dep_groups;          // > 0: groups per pair of the coarser level, which a group waits for
     float4* dbg;             // optional [batch][nlev][npts] (npx, npy, iters, status) at level end
     int dbg_pt;              // point whose per-iteration values are appended after dbg (pair 0)
 };
+
+// LK counters (queue heads per level and XCD, dataflow retire counts per level and pair): one per
+// 128-B line.  Packed, a line held the counters of several levels (or pairs) that concurrently
+// running launches update and poll, and the dataflow ran 1.4-3x slower wherever the batch did not
+// fill whole lines (8, 16, 24, 40 pairs) -- the concurrent launches contending on shared lines.
+constexpr int kCtrPad = 32;
 
 // Core rows [lo, hi) of one pyramid level (row-band mode: what a band's LK reads)
 struct RowSpan {
@@ -145,15 +152,15 @@ hipError_t launch_traj_init(hipStream_t s, int npts, int ny, int pixel_step, int
 hipError_t launch_traj_update(hipStream_t s, int npts, const float* next_pts, const uint8_t* status, float* cur,
                               float* traj, int* tlen, int nimg, int w, int h, int last, double min_vector_size,
                               double* vectors, float* start_pts, int* num);
-// Ab: [nlev][batch][npts] per-point (A11, A12, A22, 1/D); qctr: [batch][kMaxLevels][8] queue
+// Ab: [nlev][batch][npts] per-point (A11, A12, A22, 1/D); qctr: [batch][kMaxLevels][8] (x kCtrPad) queue
 // heads.  aux (may be null): second stream for the flow-independent class / A kernels; ev: kMaxLevels
 // + 1 events (no timing) used to order the two streams.  prev_ready (may be null): recorded by the
 // caller once the first frames' pyramids exist; the aux work waits on it instead of on everything
 // enqueued on s so far (the second frames' pyramids may still be in flight on s).
 // Dataflow (s2 and flow_ev[2] non-null, done: kMaxLevels x batch ints): the level launches alternate
 // between s and s2, so level L-1 starts in level L's tail; its groups wait for their pair's level-L
-// groups (done counters).  Used when every XCD's work range holds whole pairs (batch % 8 == 0) and
-// pairs' next_pts do not share 128-B lines (npts % 16 == 0).
+// groups (done counters).  Used when every XCD's work range holds two or more whole pairs (batch a
+// multiple of 8, at least 16) and pairs' next_pts do not share 128-B lines (npts % 16 == 0).
 // lvl_done (may be null: calls do not overlap): [kMaxLevels] events, re-recorded after each level's
 // iteration launch; the aux stream waits for the previous call's before rewriting that level's
 // class planes, A sums and queue heads (call pipelining lets the aux stream run a call ahead).
@@ -173,9 +180,10 @@ hipError_t launch_band_fit(hipStream_t s, int nrec, const mdx_band_cand* cands, 
 // bytes of the scratch launch_classify_fit needs
 inline size_t classify_scratch_bytes(int batch, int npts) { return (size_t)batch * ((npts + 255) / 256) * 32; }
 // Row bands: frame-1 gray rows [fit->src_y0, fit->src_y1) into the padded level 0 of pyr1 (the
-// band's warp may read rows its own pyramid build skipped).  gray1_l0: level-0 core, pitch bytes.
+// band's warp may read rows its own pyramid build skipped), except the rows [built0, built1) the
+// pyramid build wrote.  gray1_l0: level-0 core, pitch bytes.
 hipError_t launch_gray_rows(hipStream_t s, const uint8_t* img1, int w, int h, int stride, int fmt, uint8_t* gray1_l0,
-                            int pitch, const PairFit* fit);
+                            int pitch, const PairFit* fit, int built0 = 0, int built1 = 0);
 hipError_t launch_set_fit_external(hipStream_t s, int batch, const double* H_external, PairFit* fits);
 // Destination rows [row0, row1) of every pair (row1 <= h); mask row y is at mask + (y - row0) * w.
 hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,

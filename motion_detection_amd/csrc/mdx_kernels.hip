@@ -1142,12 +1142,15 @@ __global__ void k_band_fit(const mdx_band_cand* __restrict__ cands, int nrec, Pa
 // Rows [fit->src_y0, fit->src_y1) of frame 1 -> gray, into the padded level-0 core (what k_front
 // writes there): block (bx, by) converts 256 columns of rows src_y0 + by, + gridDim.y, ...
 __global__ __launch_bounds__(64) void k_gray_rows(const uint8_t* __restrict__ img1, int w, int stride, int fmt,
-                                                  uint8_t* __restrict__ g, int pitch, const PairFit* __restrict__ fit)
+                                                  uint8_t* __restrict__ g, int pitch, const PairFit* __restrict__ fit,
+                                                  int built0, int built1)
 {
     const int r0 = fit->src_y0, r1 = fit->src_y1;
     const int x = (blockIdx.x * 64 + threadIdx.x) * 4;
     if (x >= w) return;
     for (int y = r0 + (int)blockIdx.y; y < r1; y += gridDim.y) {
+        if (y >= built0 && y < built1) continue;   // the band's flow built these rows
+
         const uint8_t* sp = img1 + (long long)y * stride;
         uint8_t* dp = g + (long long)y * pitch + x;
         const int n = min(4, w - x);
@@ -1162,11 +1165,11 @@ __global__ __launch_bounds__(64) void k_gray_rows(const uint8_t* __restrict__ im
 }
 
 hipError_t launch_gray_rows(hipStream_t s, const uint8_t* img1, int w, int h, int stride, int fmt, uint8_t* gray1_l0,
-                            int pitch, const PairFit* fit)
+                            int pitch, const PairFit* fit, int built0, int built1)
 {
     (void)h;
     const dim3 grid((w + 255) / 256, 64);
-    hipLaunchKernelGGL(k_gray_rows, grid, dim3(64), 0, s, img1, w, stride, fmt, gray1_l0, pitch, fit);
+    hipLaunchKernelGGL(k_gray_rows, grid, dim3(64), 0, s, img1, w, stride, fmt, gray1_l0, pitch, fit, built0, built1);
     return hipGetLastError();
 }
 

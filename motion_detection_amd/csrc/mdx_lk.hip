@@ -424,7 +424,7 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
     const int nw = gridDim.x;
     const int bid = xcd_remap(blockIdx.x + nw * blockIdx.y, nw * gridDim.y);
     const int pair = bid / nw, w = bid % nw;
-    if (bid == 0 && lane < 8) qctr[level * 8 + lane] = 0;          // k_lk_iter's queue heads
+    if (bid == 0 && lane < 8) qctr[(level * 8 + lane) * kCtrPad] = 0;   // k_lk_iter's queue heads
     const ClassLevel& C = a.plan.lv[level];
     const Level L = a.g.lv[level];
     const int g = w * S + slot;
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
     const int p0 = (int)(cb / ngroups);
     const uint32_t off0 = (uint32_t)(cb - (long long)p0 * ngroups);   // cb's group within pair p0
     const int np = ce > cb ? (int)((ce - 1) / ngroups) - p0 + 1 : 1;
-    int* ctr = qctr + level * 8 + xcd;
+    int* ctr = qctr + (level * 8 + xcd) * kCtrPad;
     const ClassLevel& C = a.plan.lv[level];
     const Level L = a.g.lv[level];
     // buffer addressing: descriptors over the range's class slabs and next-frame pyramids (the
@@ -604,7 +604,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
             // stores, vmcnt(0), agent atomic; the reader polls and loads sc1)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (sl == 0)
-                __hip_atomic_fetch_add(a.done + level * a.done_stride + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(a.done + (level * a.done_stride + pair) * kCtrPad, 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
         }
     };
 
@@ -644,13 +645,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                             // this pair has retired there (bounded: its waves are resident and
                             // drain their queue), then read the carried points past L1
                             if (sl == 0 && !gave_up) {
-                                const int* d = a.done + (level + 1) * a.done_stride + pair;
-                                int t = 0;
-                                for (; t < kLkSpinMax; t++) {
-                                    if (__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.dep_groups) break;
-                                    __builtin_amdgcn_s_sleep(8);
+                                // polls back off (1 .. 16 sleeps between loads): thousands of
+                                // waiting waves polling one line would load its L2 channel
+                                const int* d = a.done + ((level + 1) * a.done_stride + pair) * kCtrPad;
+                                int slept = 0, gap = 1;
+                                while (__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.dep_groups) {
+                                    if (slept >= kLkSpinMax) {
+                                        gave_up = true;
+                                        break;
+                                    }
+                                    for (int i = 0; i < gap; i++) __builtin_amdgcn_s_sleep(8);
+                                    slept += gap;
+                                    gap = gap < 16 ? 2 * gap : 16;
                                 }
-                                if (t == kLkSpinMax) gave_up = true;
                             }
                             if (q.valid)
                                 p = __builtin_bit_cast(float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(a.next_pts) + po,
@@ -869,18 +876,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
 }
 
 // Dataflow gate: one wave, launched on the next level's stream right before that level's
-// iteration launch, returns once every XCD's queue of `level` (T groups in 8 ranges) has been
-// handed out -- the start of that level's tail.  The next level's persistent waves are then
-// dispatched only into the slots the tail frees; launched while the level still had its whole
-// queue ahead, they took half the chip and spun there (both launches ~2x slower, measured).
-// Bounded like the group waits (~0.1 s).
-__global__ __launch_bounds__(64) void k_lk_gate(const int* __restrict__ qctr, long long T)
+// iteration launch.  It returns once, on every XCD, the coarser level's queue has been handed out
+// (the start of its tail) and the first pair of the XCD's next-level range has finished the
+// coarser level (its first groups can run at once).  The next level's persistent waves are then
+// dispatched only into the slots the tail frees, and find ready work there.  Without the gate the
+// next level, launched beside the coarser level's whole queue, took half the chip and spun (both
+// launches ~2x slower); gated on the queues alone, one pair per XCD (4K x 8) left every next-level
+// wave polling its pair's counter (LK 3x slower).  Bounded like the group waits.
+__global__ __launch_bounds__(64) void k_lk_gate(const int* __restrict__ qctr, long long T, const int* __restrict__ done,
+                                                int dep_groups, int ngroups_next, long long T_next)
 {
     const int x = threadIdx.x;
     if (x >= 8) return;
     const long long cb = T * x / 8, ce = T * (x + 1) / 8;
+    const long long cbn = T_next * x / 8;
+    const int pf = cbn < T_next ? (int)(cbn / ngroups_next) : -1;
     for (int t = 0; t < kLkSpinMax; t++) {
-        if (__hip_atomic_load(qctr + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ce - cb) break;
+        const bool dry = __hip_atomic_load(qctr + x * kCtrPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ce - cb;
+        const bool first =
+            pf < 0 || __hip_atomic_load(done + pf * kCtrPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= dep_groups;
+        if (dry && first) break;
         __builtin_amdgcn_s_sleep(8);
     }
 }
@@ -974,7 +989,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         b.status = a.status + (long long)p * a.npts;
         if (p) b.dbg = nullptr;   // the trace covers the first sub-batch
         uint8_t* bcls = cls + (long long)p * a.plan.bytes_per_pair;
-        int* bq = qctr + si * kMaxLevels * 8;
+        int* bq = qctr + si * kMaxLevels * 8 * kCtrPad;
         if (aux) {
             hipEvent_t ready = prev_ready;
             if (!ready || p) {   // later sub-batches follow everything on s (their slabs are reused)
@@ -1019,11 +1034,13 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             }
         }
         // dataflow: every XCD's work range must hold whole pairs (the hand-off stays in one L2) and
-        // no two pairs' carried points may share a 128-B line
-        const bool flow = aux && s2 && flow_ev && done && !b.dbg && nb % 8 == 0 && a.npts % 16 == 0 &&
+        // no two pairs' carried points may share a 128-B line; with one pair per XCD (batch 8) the
+        // next level can only start once the whole level is done there, and the dataflow measured
+        // 1.5% slower than levels in sequence, so it needs at least two
+        const bool flow = aux && s2 && flow_ev && done && !b.dbg && nb % 8 == 0 && nb >= 16 && a.npts % 16 == 0 &&
                           (reinterpret_cast<uintptr_t>(b.next_pts) & 127) == 0;
         if (flow) {
-            if (hipError_t e = hipMemsetAsync(done, 0, sizeof(int) * kMaxLevels * nb, s)) return e;
+            if (hipError_t e = hipMemsetAsync(done, 0, sizeof(int) * kMaxLevels * nb * kCtrPad, s)) return e;
             if (hipError_t e = hipEventRecord(flow_ev[0], s)) return e;   // counters zeroed, front end done
             if (hipError_t e = hipStreamWaitEvent(s2, flow_ev[0], 0)) return e;
         }
@@ -1044,7 +1061,10 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
                 bl.dep_groups = (Cp.nxp / Cp.G) * a.nyg;
             }
             if (bl.dep_groups) {   // start in the coarser level's tail, not beside its whole queue
-                hipLaunchKernelGGL(k_lk_gate, dim3(1), dim3(64), 0, st, bq + (l + 1) * 8, (long long)nb * bl.dep_groups);
+                const int ng = (C.nxp / C.G) * a.nyg;
+                hipLaunchKernelGGL(k_lk_gate, dim3(1), dim3(64), 0, st, bq + (l + 1) * 8 * kCtrPad,
+                                   (long long)nb * bl.dep_groups, done + (l + 1) * nb * kCtrPad, bl.dep_groups, ng,
+                                   (long long)nb * ng);
             }
             const float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             switch (C.G * 1000 + C.UW) {

@@ -159,12 +159,14 @@ def test_warp_diff_dev_batch(mdx, ctx, oracle):
     (11, {"MDX_LK_G": "4"}, (320, 240)),
     (11, {"MDX_LK_G": "8"}, (320, 240)),
     (5, {"MDX_LK_AUX": "0"}, (320, 240)),   # class / A kernels on the main stream
-    # LK dataflow (batch a multiple of 8, npts a multiple of 16): level l-1's launch overlaps
-    # level l's and waits per pair; per sub-batch; off; group size 8 everywhere; a larger frame
-    (8, {}, (320, 240)),
-    (16, {"MDX_LK_SUB": "8"}, (320, 240)),
-    (8, {"MDX_LK_FLOW": "0"}, (320, 240)),
-    (8, {"MDX_LK_G": "8"}, (320, 240)),
+    # LK dataflow (batch a multiple of 8 and >= 16, npts a multiple of 16): level l-1's launch
+    # overlaps level l's and waits per pair; per sub-batch; off; group size 8 everywhere; a larger
+    # frame; 24 pairs (three per XCD)
+    (16, {}, (320, 240)),
+    (32, {"MDX_LK_SUB": "16"}, (320, 240)),
+    (24, {}, (320, 240)),
+    (16, {"MDX_LK_FLOW": "0"}, (320, 240)),
+    (16, {"MDX_LK_G": "8"}, (320, 240)),
     (16, {}, (640, 480)),
 ])
 def test_batch_dev_matches_host_path(mdx, oracle, monkeypatch, B, env, wh):
