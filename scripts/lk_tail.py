@@ -45,9 +45,10 @@ def main():
     s_all, e_all = t0[:nlev][ok_all].astype(np.int64), t1[:nlev][ok_all].astype(np.int64)
     if len(s_all):
         span_all = (e_all.max() - s_all.min()) * 10
-        cap = max(int(ok_all.sum(axis=1).max()), 1)
+        # k_lk_iter's resident capacity on MI355X: 256 CUs x 4 SIMDs x 4 waves (<= 128 VGPRs)
+        cap = 4096
         use = ((e_all - s_all) * 10).sum() / (cap * span_all)
-        print(f"all levels: span {span_all / 1e3:.0f} us, wave-time / (widest launch {cap} waves x span) {use:.3f}")
+        print(f"all levels: span {span_all / 1e3:.0f} us, wave-time / ({cap} resident waves x span) {use:.3f}")
     for L in range(nlev - 1, -1, -1):
         ok = t1[L] > 0
         s, e = t0[L][ok].astype(np.int64), t1[L][ok].astype(np.int64)
