@@ -1037,7 +1037,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         // no two pairs' carried points may share a 128-B line; with one pair per XCD (batch 8) the
         // next level can only start once the whole level is done there, and the dataflow measured
         // 1.5% slower than levels in sequence, so it needs at least two
-        const bool flow = aux && s2 && flow_ev && done && !b.dbg && nb % 8 == 0 && nb >= 16 && a.npts % 16 == 0 &&
+        const bool flow = aux && s2 && flow_ev && done && nb % 8 == 0 && nb >= 16 && a.npts % 16 == 0 &&
                           (reinterpret_cast<uintptr_t>(b.next_pts) & 127) == 0;
         if (flow) {
             if (hipError_t e = hipMemsetAsync(done, 0, sizeof(int) * kMaxLevels * nb * kCtrPad, s)) return e;
