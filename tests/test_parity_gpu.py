@@ -216,11 +216,15 @@ def test_reference_interface(mdx, oracle):
     ofc.close()
 
 
-@pytest.mark.parametrize("w,h,ps,nb,ch", [(640, 480, 10, 3, 1), (333, 241, 7, 5, 1), (1920, 1080, 10, 8, 1),
-                                          (640, 480, 3, 2, 3), (320, 240, 10, 1, 1), (7680, 4320, 10, 8, 3)])
-def test_row_tiled_matches_full(mdx, w, h, ps, nb, ch):
+@pytest.mark.parametrize("w,h,ps,nb,ch,pipe", [(640, 480, 10, 3, 1, "0"), (333, 241, 7, 5, 1, "0"),
+                                               (1920, 1080, 10, 8, 1, "0"), (640, 480, 3, 2, 3, "0"),
+                                               (320, 240, 10, 1, 1, "0"), (7680, 4320, 10, 8, 3, "0"),
+                                               (640, 480, 3, 2, 3, "1"), (1920, 1080, 10, 8, 1, "1")])
+def test_row_tiled_matches_full(mdx, monkeypatch, w, h, ps, nb, ch, pipe):
     """Row bands run one after another on one GPU, records exchanged through
-    host memory: every point, the fit, the count and every mask row equal the full path's."""
+    host memory: every point, the fit, the count and every mask row equal the full path's (also
+    with call pipelining, whose band calls alternate pyramid halves)."""
+    monkeypatch.setenv("MDX_PIPE", pipe)
     from motion_detection_amd import rowtile
     a, b, _ = mdx.synth_pair(7000 + nb, w, h, ch)
     fmt = mdx.FMT_GRAY8 if ch == 1 else mdx.FMT_RGB8
@@ -358,11 +362,13 @@ def test_back_to_back_calls_pipelined(mdx, oracle, monkeypatch, env):
             np.testing.assert_array_equal(got[j]["mask"][i], ref["mask"])
 
 
-@pytest.mark.parametrize("w,h,ps,nb,ch", [(640, 480, 10, 4, 1), (1280, 720, 7, 3, 3)])
-def test_row_bands_on_separate_contexts(mdx, w, h, ps, nb, ch):
+@pytest.mark.parametrize("w,h,ps,nb,ch,pipe", [(640, 480, 10, 4, 1, "0"), (1280, 720, 7, 3, 3, "0"),
+                                               (640, 480, 10, 4, 1, "1")])
+def test_row_bands_on_separate_contexts(mdx, monkeypatch, w, h, ps, nb, ch, pipe):
     """Each band on its own context, as on its own GPU: a band's flow builds frame 1's pyramid for
     its rows only, so the rows its warp reads beyond the band (camera motion) come from the frame
-    at fit/warp time.  Every mask row equals the full path's."""
+    at fit/warp time.  Every mask row equals the full path's (also with call pipelining)."""
+    monkeypatch.setenv("MDX_PIPE", pipe)
     from motion_detection_amd import rowtile
     a, b, _ = mdx.synth_pair(7100 + nb, w, h, ch)
     fmt = mdx.FMT_GRAY8 if ch == 1 else mdx.FMT_RGB8
