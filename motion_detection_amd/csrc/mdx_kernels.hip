@@ -466,6 +466,8 @@ __global__ __launch_bounds__(256) void k_scharr(const uint8_t* __restrict__ pyr1
 // products rounded once to float) in parallel and store them chain-ordered in LDS; then one
 // lane per chain (12 chains for A11/A12/A22, 8 for b1/b2) adds its 80 terms of the chunk in
 // order.  The result is bit-identical to the x86 reference, not merely within tolerance.
+typedef short s2k __attribute__((ext_vector_type(2)));
+
 template <int LPP>
 __global__ __launch_bounds__(64) void k_lk(LkArgs a)
 {
@@ -484,15 +486,26 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a)
     float* ch = reinterpret_cast<float*>(lds4) + p * PT_FLOATS;
     float* res = ch + 12 * STRIDE;
 
-    // element geometry (level independent)
+    // element geometry (level independent).  LPP 64: lane s owns a run of 5 adjacent window
+    // columns of one row per 8-row chunk (row s >> 3, columns 5 (s & 7) .. +4), so its taps of a
+    // chunk are two 12-B row loads (J: v_perm + v_dot2 tap pairs) instead of 4 byte loads per element
+    static_assert(LPP != 64 || EC == 5, "row runs of 5");
     int woff[EC], ex[EC], ey[EC];
 #pragma unroll
     for (int i = 0; i < EC; i++) {
-        const int e = s + LPP * i;
+        const int e = LPP == 64 ? (s >> 3) * WIN + 5 * (s & 7) + i : s + LPP * i;
         ey[i] = e / WIN;
         ex[i] = e % WIN;
         woff[i] = (ex[i] & 3) * STRIDE + ey[i] * 10 + (ex[i] >> 2);
     }
+    // 12 bytes of a row from byte address p, realigned: (lo, hi) = bytes p .. p+7
+    auto row8 = [](const uint8_t* p, uint32_t& lo, uint32_t& hi) {
+        const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+        const u3a4k v = *reinterpret_cast<const u3a4k*>(u & ~(uintptr_t)3);
+        const uint32_t o = (uint32_t)(u & 3);
+        lo = __builtin_amdgcn_alignbyte(v.y, v.x, o);
+        hi = __builtin_amdgcn_alignbyte(v.z, v.y, o);
+    };
 
     const int gx = valid ? pt / a.ny : 0, gy = valid ? pt % a.ny : 0;
     float px0 = (float)(gx * a.pixel_step), py0 = (float)(gy * a.pixel_step);
@@ -546,25 +559,65 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a)
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             if (ok) {
+                // LPP 64: the run's I bytes and derivative words of both tap rows, vector loads
+                uint64_t r0 = 0, r1 = 0;
+                uint32_t dr0[6] = {}, dr1[6] = {};
+                if constexpr (LPP == 64) {
+                    const int o = ibase + c * R * pitch + toff[0];
+                    uint32_t l0, h0, l1, h1;
+                    row8(Ib + o, l0, h0);
+                    row8(Ib + o + pitch, l1, h1);
+                    r0 = ((uint64_t)h0 << 32) | l0;
+                    r1 = ((uint64_t)h1 << 32) | l1;
+                    const uint32_t* dp = Db + o;
+                    const u4a4k a0 = *reinterpret_cast<const u4a4k*>(dp);
+                    const u2a4k b0 = *reinterpret_cast<const u2a4k*>(dp + 4);
+                    const u4a4k a1 = *reinterpret_cast<const u4a4k*>(dp + pitch);
+                    const u2a4k b1 = *reinterpret_cast<const u2a4k*>(dp + pitch + 4);
+                    dr0[0] = a0.x; dr0[1] = a0.y; dr0[2] = a0.z; dr0[3] = a0.w; dr0[4] = b0.x; dr0[5] = b0.y;
+                    dr1[0] = a1.x; dr1[1] = a1.y; dr1[2] = a1.z; dr1[3] = a1.w; dr1[4] = b1.x; dr1[5] = b1.y;
+                }
 #pragma unroll
                 for (int i = 0; i < EC; i++) {
                     const int o = ibase + c * R * pitch + toff[i];
                     const uint8_t* ip = Ib + o;
-                    const int ival = (ip[0] * w00 + ip[1] * w01 + ip[pitch] * w10 + ip[pitch + 1] * w11 + 256) >> 9;
                     const uint32_t* dp = Db + o;
-                    const uint32_t d00 = dp[0], d01 = dp[1], d10 = dp[pitch], d11 = dp[pitch + 1];
-                    const int ixv = ((int)(int16_t)d00 * w00 + (int)(int16_t)d01 * w01 + (int)(int16_t)d10 * w10 +
-                                     (int)(int16_t)d11 * w11 + 8192) >> 14;
-                    const int iyv = (((int)d00 >> 16) * w00 + ((int)d01 >> 16) * w01 + ((int)d10 >> 16) * w10 +
-                                     ((int)d11 >> 16) * w11 + 8192) >> 14;
+                    int ival;
+                    uint32_t d00, d01, d10, d11;
+                    int ixv, iyv;
+                    if constexpr (LPP == 64) {
+                        // the same integer sums as below through v_dot2 on 16-bit pairs (tap bytes,
+                        // Ix / Iy halves; signed weights), no 32-bit multiplies
+                        const s2k W0 = {(short)w00, (short)w01}, W1 = {(short)w10, (short)w11};
+                        const unsigned sel = 0x0c000c00u | (unsigned)i | ((unsigned)(i + 1) << 16);
+                        const s2k t0 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm((uint32_t)(r0 >> 32), (uint32_t)r0, sel));
+                        const s2k t1 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm((uint32_t)(r1 >> 32), (uint32_t)r1, sel));
+                        ival = __builtin_amdgcn_sdot2(t0, W0, __builtin_amdgcn_sdot2(t1, W1, 256, false), false) >> 9;
+                        d00 = dr0[i]; d01 = dr0[i + 1]; d10 = dr1[i]; d11 = dr1[i + 1];
+                        const s2k x0 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(d01, d00, 0x05040100u));
+                        const s2k x1 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(d11, d10, 0x05040100u));
+                        const s2k y0 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(d01, d00, 0x07060302u));
+                        const s2k y1 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(d11, d10, 0x07060302u));
+                        ixv = __builtin_amdgcn_sdot2(x0, W0, __builtin_amdgcn_sdot2(x1, W1, 8192, false), false) >> 14;
+                        iyv = __builtin_amdgcn_sdot2(y0, W0, __builtin_amdgcn_sdot2(y1, W1, 8192, false), false) >> 14;
+                    } else {
+                        ival = (ip[0] * w00 + ip[1] * w01 + ip[pitch] * w10 + ip[pitch + 1] * w11 + 256) >> 9;
+                        d00 = dp[0]; d01 = dp[1]; d10 = dp[pitch]; d11 = dp[pitch + 1];
+                        ixv = ((int)(int16_t)d00 * w00 + (int)(int16_t)d01 * w01 + (int)(int16_t)d10 * w10 +
+                               (int)(int16_t)d11 * w11 + 8192) >> 14;
+                        iyv = (((int)d00 >> 16) * w00 + ((int)d01 >> 16) * w01 + ((int)d10 >> 16) * w10 +
+                               ((int)d11 >> 16) * w11 + 8192) >> 14;
+                    }
                     const int k = c * EC + i;
                     sd[k] = ((uint32_t)ixv & 0xffffu) | ((uint32_t)iyv << 16);
                     if (k & 1) si[k >> 1] = (si[k >> 1] & 0xffffu) | ((uint32_t)ival << 16);
                     else si[k >> 1] = (uint32_t)ival;
                     float* wp = ch + woff[i];
-                    wp[0] = (float)(ixv * ixv);
-                    wp[4 * STRIDE] = (float)(ixv * iyv);
-                    wp[8 * STRIDE] = (float)(iyv * iyv);
+                    // |Ix|, |Iy| <= 4080: 24-bit multiplies (v_mul_i32_i24, full rate; a 32-bit
+                    // v_mul_lo_u32 is quarter rate), products exact in int32
+                    wp[0] = (float)__mul24(ixv, ixv);
+                    wp[4 * STRIDE] = (float)__mul24(ixv, iyv);
+                    wp[8 * STRIDE] = (float)__mul24(iyv, iyv);
                 }
             }
             __syncthreads();
@@ -629,17 +682,35 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a)
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
                 if (act) {
+                    uint32_t j0l = 0, j0h = 0, j1l = 0, j1h = 0;
+                    if constexpr (LPP == 64) {
+                        const uint8_t* jp = Jb + (jbase + c * R * pitch + toff[0]);
+                        row8(jp, j0l, j0h);
+                        row8(jp + pitch, j1l, j1h);
+                    }
 #pragma unroll
                     for (int i = 0; i < EC; i++) {
-                        const uint8_t* jp = Jb + (jbase + c * R * pitch + toff[i]);
-                        const int jv = (jp[0] * v00 + jp[1] * v01 + jp[pitch] * v10 + jp[pitch + 1] * v11 + 256) >> 9;
+                        int jv;
+                        if constexpr (LPP == 64) {
+                            // (J[x], J[x+1]) of both tap rows as 16-bit pairs; v_dot2 gives the
+                            // reference's int sum j00*v00 + j01*v01 + j10*v10 + j11*v11 exactly
+                            const unsigned sel = 0x0c000c00u | (unsigned)i | ((unsigned)(i + 1) << 16);
+                            const s2k t0 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(j0h, j0l, sel));
+                            const s2k t1 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(j1h, j1l, sel));
+                            const s2k W0 = {(short)v00, (short)v01}, W1 = {(short)v10, (short)v11};
+                            jv = __builtin_amdgcn_sdot2(t0, W0, __builtin_amdgcn_sdot2(t1, W1, 256, false), false) >> 9;
+                        } else {
+                            const uint8_t* jp = Jb + (jbase + c * R * pitch + toff[i]);
+                            jv = (jp[0] * v00 + jp[1] * v01 + jp[pitch] * v10 + jp[pitch + 1] * v11 + 256) >> 9;
+                        }
                         const int k = c * EC + i;
                         const int iv = (k & 1) ? (int)(si[k >> 1] >> 16) : (int)(si[k >> 1] & 0xffffu);
                         const int diff = jv - iv;
                         const uint32_t dv = sd[k];
                         float* wp = ch + woff[i];
-                        wp[0] = (float)(diff * (int)(int16_t)dv);
-                        wp[4 * STRIDE] = (float)(diff * ((int)dv >> 16));
+                        // |diff| <= 8160, |Ix|, |Iy| <= 4080: exact 24-bit multiplies
+                        wp[0] = (float)__mul24(diff, (int)(int16_t)dv);
+                        wp[4 * STRIDE] = (float)__mul24(diff, (int)dv >> 16);
                     }
                 }
                 __syncthreads();
