@@ -83,6 +83,29 @@ __device__ __forceinline__ void lk_weights(float fa, float fb, int& w00, int& w0
     w11 = 16384 - w00 - w01 - w10;
 }
 
+// The window element of one class / point at a pixel: LKTrackerInvoker's integer sums
+//   I*32 = (i00 w00 + i01 w01 + i10 w10 + i11 w11 + 256) >> 9,  Ix/Iy = (sum d w + 8192) >> 14,
+// evaluated with v_dot2 on 16-bit pairs (tap bytes, Ix / Iy halves; signed weights, w11 may be -1)
+// -- the same int32 sums without any 32-bit multiply (v_mul_lo_u32 is quarter rate).  (lo, hi)
+// hold the bytes of the tap rows y / y+1 with taps at bytes Q, Q+1; d* are the derivative words.
+template <int Q>
+__device__ __forceinline__ void lk_interp(uint32_t lo0, uint32_t hi0, uint32_t lo1, uint32_t hi1, uint32_t d00,
+                                          uint32_t d01, uint32_t d10, uint32_t d11, s2 W0, s2 W1, int& ival, int& ixv,
+                                          int& iyv)
+{
+    static_assert(Q >= 0 && Q < 7, "tap byte");
+    constexpr unsigned sel = 0x0c000c00u | (unsigned)Q | ((unsigned)(Q + 1) << 16);
+    const s2 t0 = __builtin_bit_cast(s2, __builtin_amdgcn_perm(hi0, lo0, sel));
+    const s2 t1 = __builtin_bit_cast(s2, __builtin_amdgcn_perm(hi1, lo1, sel));
+    ival = __builtin_amdgcn_sdot2(t0, W0, __builtin_amdgcn_sdot2(t1, W1, 256, false), false) >> 9;
+    const s2 x0 = __builtin_bit_cast(s2, __builtin_amdgcn_perm(d01, d00, 0x05040100u));
+    const s2 x1 = __builtin_bit_cast(s2, __builtin_amdgcn_perm(d11, d10, 0x05040100u));
+    const s2 y0 = __builtin_bit_cast(s2, __builtin_amdgcn_perm(d01, d00, 0x07060302u));
+    const s2 y1 = __builtin_bit_cast(s2, __builtin_amdgcn_perm(d11, d10, 0x07060302u));
+    ixv = __builtin_amdgcn_sdot2(x0, W0, __builtin_amdgcn_sdot2(x1, W1, 8192, false), false) >> 14;
+    iyv = __builtin_amdgcn_sdot2(y0, W0, __builtin_amdgcn_sdot2(y1, W1, 8192, false), false) >> 14;
+}
+
 // broadcast lane j of this lane's quad (DPP quad_perm, no LDS)
 template <int J>
 __device__ __forceinline__ float quad_bcast(float v)
@@ -223,20 +246,16 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
             dw[r][0] = d4.x; dw[r][1] = d4.y; dw[r][2] = d4.z; dw[r][3] = d4.w;
             dw[r][4] = dp[(long long)r * p + 4];
         }
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (x0 + q >= L.w + kPad - 1) { cv[q] = 256; continue; }
-            const int i00 = (ib[0][q >> 2] >> (8 * (q & 3))) & 255, i01 = (ib[0][(q + 1) >> 2] >> (8 * ((q + 1) & 3))) & 255;
-            const int i10 = (ib[1][q >> 2] >> (8 * (q & 3))) & 255, i11 = (ib[1][(q + 1) >> 2] >> (8 * ((q + 1) & 3))) & 255;
-            const int ival = (i00 * w00 + i01 * w01 + i10 * w10 + i11 * w11 + 256) >> 9;
-            const uint32_t d00 = dw[0][q], d01 = dw[0][q + 1], d10 = dw[1][q], d11 = dw[1][q + 1];
-            const int ixv = ((int)(int16_t)d00 * w00 + (int)(int16_t)d01 * w01 + (int)(int16_t)d10 * w10 +
-                             (int)(int16_t)d11 * w11 + 8192) >> 14;
-            const int iyv = (((int)d00 >> 16) * w00 + ((int)d01 >> 16) * w01 + ((int)d10 >> 16) * w10 +
-                             ((int)d11 >> 16) * w11 + 8192) >> 14;
+        const s2 W0 = {(short)w00, (short)w01}, W1 = {(short)w10, (short)w11};
+        static_for<0, 4>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            if (x0 + q >= L.w + kPad - 1) { cv[q] = 256; return; }
+            int ival, ixv, iyv;
+            lk_interp<q>(ib[0][0], ib[0][1], ib[1][0], ib[1][1], dw[0][q], dw[0][q + 1], dw[1][q], dw[1][q + 1], W0, W1,
+                         ival, ixv, iyv);
             dv[q] = ((uint32_t)ixv & 0xffffu) | ((uint32_t)iyv << 16);
             cv[q] = 256 - 512 * ival;   // J-chain bias: (S + C) >> 9 == ((S + 256) >> 9) - I
-        }
+        });
     } else {
 #pragma unroll
         for (int q = 0; q < 4; q++) cv[q] = 256;
@@ -313,20 +332,17 @@ __global__ __launch_bounds__(256) void k_lk_class_fused(const uint8_t* __restric
         uint32_t dv[4] = {0, 0, 0, 0};
         int cv[4] = {256, 256, 256, 256};
         if (inside) {
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (x0 + q >= L.w + kPad - 1) continue;
-                const int i00 = u8_at(rw[1], 4 + q), i01 = u8_at(rw[1], 5 + q);
-                const int i10 = u8_at(rw[2], 4 + q), i11 = u8_at(rw[2], 5 + q);
-                const int ival = (i00 * w00 + i01 * w01 + i10 * w10 + i11 * w11 + 256) >> 9;
-                const uint32_t d00 = dw[0][q], d01 = dw[0][q + 1], d10 = dw[1][q], d11 = dw[1][q + 1];
-                const int ixv = ((int)(int16_t)d00 * w00 + (int)(int16_t)d01 * w01 + (int)(int16_t)d10 * w10 +
-                                 (int)(int16_t)d11 * w11 + 8192) >> 14;
-                const int iyv = (((int)d00 >> 16) * w00 + ((int)d01 >> 16) * w01 + ((int)d10 >> 16) * w10 +
-                                 ((int)d11 >> 16) * w11 + 8192) >> 14;
+            const s2 W0 = {(short)w00, (short)w01}, W1 = {(short)w10, (short)w11};
+            static_for<0, 4>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                if (x0 + q >= L.w + kPad - 1) return;
+                int ival, ixv, iyv;
+                // taps at bytes 4+q, 5+q of rows y / y+1 (rw[1], rw[2]): bytes q, q+1 of words 1..2
+                lk_interp<q>(rw[1][1], rw[1][2], rw[2][1], rw[2][2], dw[0][q], dw[0][q + 1], dw[1][q], dw[1][q + 1], W0,
+                             W1, ival, ixv, iyv);
                 dv[q] = ((uint32_t)ixv & 0xffffu) | ((uint32_t)iyv << 16);
                 cv[q] = 256 - 512 * ival;
-            }
+            });
         }
         uint8_t* base = cls_out + (long long)pair * a.plan.bytes_per_pair + C.off + (long long)cls * C.class_bytes;
         uint4* o = reinterpret_cast<uint4*>(base) + ((long long)v * C.PW + 4 * j) / 2;
