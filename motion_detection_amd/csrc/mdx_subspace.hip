@@ -19,6 +19,8 @@
 // subspace_residual) operation for operation, un-fused, so both round identically.
 #include "mdx_internal.h"
 
+#include <algorithm>
+
 namespace mdx {
 
 constexpr int kMaxSub = 32;   // n = 2 * trajectory length (reference: 10 / 14 / 18 for 2..4 motions)
@@ -59,31 +61,40 @@ __global__ __launch_bounds__(256) void k_subspace_prep(const float* __restrict__
             int i = 0;
             if (base == 0) { acc = sv[0]; i = 1; }
             for (; i < m && (i & 3); i++) fadd(acc, sv[i]);
-            if (i + 16 <= m) {
-                float4 v4[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) v4[k] = reinterpret_cast<const float4*>(sv + i)[k];
-                for (; i + 32 <= m; i += 16) {
-                    float4 n4[4];
-#pragma unroll
-                    for (int k = 0; k < 4; k++) n4[k] = reinterpret_cast<const float4*>(sv + i + 16)[k];
-#pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        fadd(acc, v4[k].x);
-                        fadd(acc, v4[k].y);
-                        fadd(acc, v4[k].z);
-                        fadd(acc, v4[k].w);
-                        v4[k] = n4[k];
-                    }
-                }
+            auto add16 = [&](const float4 (&v)[4]) {
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    fadd(acc, v4[k].x);
-                    fadd(acc, v4[k].y);
-                    fadd(acc, v4[k].z);
-                    fadd(acc, v4[k].w);
+                    fadd(acc, v[k].x);
+                    fadd(acc, v[k].y);
+                    fadd(acc, v[k].z);
+                    fadd(acc, v[k].w);
                 }
-                i += 16;
+            };
+            auto ld16 = [&](float4 (&v)[4], int at) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) v[k] = reinterpret_cast<const float4*>(sv + at)[k];
+            };
+            if (i + 32 <= m) {
+                // two blocks of 16 in flight ahead of the adds (one block ahead left each block's
+                // LDS latency exposed: ~20 cycles per dependent add)
+                float4 a4[4], b4[4], c4[4];
+                ld16(a4, i);
+                ld16(b4, i + 16);
+                for (; i + 48 <= m; i += 48) {
+                    ld16(c4, i + 32);
+                    add16(a4);
+                    if (i + 64 > m) { add16(b4); add16(c4); i += 48; goto drained; }
+                    ld16(a4, i + 48);
+                    add16(b4);
+                    if (i + 80 > m) { add16(c4); add16(a4); i += 64; goto drained; }
+                    ld16(b4, i + 64);
+                    add16(c4);
+                }
+                // a4, b4 loaded (blocks at i, i + 16), fewer than 16 more after them
+                add16(a4);
+                add16(b4);
+                i += 32;
+            drained:;
             }
             for (; i < m; i++) fadd(acc, sv[i]);
             if (tid) ys = acc;
@@ -118,30 +129,49 @@ __global__ __launch_bounds__(256) void k_subspace_center(const float* __restrict
     }
 }
 
-// Householder QR of the n x d sample and the last n - d columns of Q (see the oracle's
-// subspace_basis for the statement); A, V column-major with leading dimension n.
-__device__ void subspace_basis(double* A, int n, int d, double* V, double* beta, double* q2)
+// Householder QR of the n x d sample and the last n - d columns of Q (the oracle's subspace_basis
+// statement for statement); A, V column-major with leading dimension n.
+// The same statements on the 64 lanes of one wave: lane 0 forms each reflector (norm, v, beta) as
+// above, then every lane applies it to its own columns c = k + lane, k + lane + 64, ... and
+// builds its own columns of Q2 -- each column's dot product and update in the order above, so
+// the results are identical; only the independent columns run side by side (the factorisation
+// by one lane was the hypothesis kernel's serial critical path).  A wave's LDS accesses complete
+// in order; the fences keep the compiler from moving them across the hand-offs.
+__device__ __forceinline__ void lane_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ void subspace_basis_wave(double* A, int n, int d, double* V, double* beta, double* q2, int lane)
 {
     for (int k = 0; k < d; k++) {
-        double nrm2 = 0.0;
-        for (int r = k; r < n; r++) nrm2 = nrm2 + A[k * n + r] * A[k * n + r];
-        const double nrm = __builtin_sqrt(nrm2);
-        const double x0 = A[k * n + k];
-        const double alpha = x0 >= 0.0 ? -nrm : nrm;
-        for (int r = k; r < n; r++) V[k * n + r] = A[k * n + r];
-        V[k * n + k] = x0 - alpha;
-        double b = 0.0;
-        for (int r = k; r < n; r++) b = b + V[k * n + r] * V[k * n + r];
-        beta[k] = b;
-        if (b == 0.0) continue;
-        for (int c = k; c < d; c++) {
-            double dot = 0.0;
-            for (int r = k; r < n; r++) dot = dot + V[k * n + r] * A[c * n + r];
-            const double f = 2.0 * dot / b;
-            for (int r = k; r < n; r++) A[c * n + r] = A[c * n + r] - f * V[k * n + r];
+        if (lane == 0) {
+            double nrm2 = 0.0;
+            for (int r = k; r < n; r++) nrm2 = nrm2 + A[k * n + r] * A[k * n + r];
+            const double nrm = __builtin_sqrt(nrm2);
+            const double x0 = A[k * n + k];
+            const double alpha = x0 >= 0.0 ? -nrm : nrm;
+            for (int r = k; r < n; r++) V[k * n + r] = A[k * n + r];
+            V[k * n + k] = x0 - alpha;
+            double b = 0.0;
+            for (int r = k; r < n; r++) b = b + V[k * n + r] * V[k * n + r];
+            beta[k] = b;
         }
+        lane_lds_sync();
+        const double b = beta[k];
+        if (b != 0.0) {
+            for (int c = k + lane; c < d; c += 64) {
+                double dot = 0.0;
+                for (int r = k; r < n; r++) dot = dot + V[k * n + r] * A[c * n + r];
+                const double f = 2.0 * dot / b;
+                for (int r = k; r < n; r++) A[c * n + r] = A[c * n + r] - f * V[k * n + r];
+            }
+        }
+        lane_lds_sync();
     }
-    for (int j = d; j < n; j++) {
+    for (int j = d + lane; j < n; j += 64) {
         double* q = q2 + (j - d) * n;
         for (int r = 0; r < n; r++) q[r] = r == j ? 1.0 : 0.0;
         for (int k = d - 1; k >= 0; k--) {
@@ -227,6 +257,7 @@ __global__ __launch_bounds__(256) void k_subspace_hyp_f32(const float* __restric
     __shared__ float sP[kMaxSub * kMaxSub];
     __shared__ int s_cnt[4];
     const int h = blockIdx.x, tid = threadIdx.x;
+    const int i0 = (int)((long long)N * blockIdx.y / gridDim.y), i1 = (int)((long long)N * (blockIdx.y + 1) / gridDim.y);
     for (int e = tid; e < n * d; e += 256) {
         const int k = e / n, r = e - k * n;
         sA[e] = data[(long long)cols[h * d + k] * n + r];
@@ -234,14 +265,15 @@ __global__ __launch_bounds__(256) void k_subspace_hyp_f32(const float* __restric
     __syncthreads();
     if (tid == 0) subspace_pnd_f32(sA, n, d, sV, sbeta, sq, sP);
     __syncthreads();
-    for (int e = tid; e < n * n; e += 256) pbuf[(long long)h * n * n + e] = sP[e];
+    if (blockIdx.y == 0)
+        for (int e = tid; e < n * n; e += 256) pbuf[(long long)h * n * n + e] = sP[e];
     int cnt = 0;
-    for (int i = tid; i < N; i += 256)
+    for (int i = i0 + tid; i < i1; i += 256)
         if ((double)subspace_residual_f32(sP, n, data + (long long)i * n) < inlier_thr) cnt++;
     for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
     if ((tid & 63) == 0) s_cnt[tid >> 6] = cnt;
     __syncthreads();
-    if (tid == 0) counts[h] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    if (tid == 0) atomicAdd(counts + h, s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3]);
 }
 
 __global__ __launch_bounds__(256) void k_subspace_final_f32(const float* __restrict__ data, int N, int n, int nhyp,
@@ -272,21 +304,23 @@ __global__ __launch_bounds__(256) void k_subspace_hyp(const float* __restrict__ 
     __shared__ double sq[kMaxSub * kMaxSub];
     __shared__ int s_cnt[4];
     const int h = blockIdx.x, tid = threadIdx.x, m = n - d;
+    const int i0 = (int)((long long)N * blockIdx.y / gridDim.y), i1 = (int)((long long)N * (blockIdx.y + 1) / gridDim.y);
     for (int e = tid; e < n * d; e += 256) {
         const int k = e / n, r = e - k * n;
         sA[e] = (double)data[(long long)cols[h * d + k] * n + r];
     }
     __syncthreads();
-    if (tid == 0) subspace_basis(sA, n, d, sV, sbeta, sq);
+    if (tid < 64) subspace_basis_wave(sA, n, d, sV, sbeta, sq, tid);
     __syncthreads();
-    for (int e = tid; e < n * m; e += 256) qbuf[(long long)h * n * m + e] = sq[e];
+    if (blockIdx.y == 0)
+        for (int e = tid; e < n * m; e += 256) qbuf[(long long)h * n * m + e] = sq[e];
     int cnt = 0;
-    for (int i = tid; i < N; i += 256)
+    for (int i = i0 + tid; i < i1; i += 256)
         if (subspace_residual(sq, n, m, data + (long long)i * n) < inlier_thr) cnt++;
     for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o);
     if ((tid & 63) == 0) s_cnt[tid >> 6] = cnt;
     __syncthreads();
-    if (tid == 0) counts[h] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    if (tid == 0) atomicAdd(counts + h, s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3]);
 }
 
 // Winner = the first hypothesis with the largest positive count; its residual per trajectory and
@@ -325,15 +359,20 @@ hipError_t launch_subspace(hipStream_t s, const float* traj, int N, int T, int d
     float* mean = data + (size_t)N * n;
     hipLaunchKernelGGL(k_subspace_prep, dim3(1), dim3(256), 0, s, traj, N, T, mean);
     hipLaunchKernelGGL(k_subspace_center, dim3((N + 255) / 256), dim3(256), 0, s, traj, N, n, mean, data);
+    // every hypothesis over S slices of the trajectories (one workgroup each, the basis recomputed per
+    // slice, inlier counts added atomically -- an order-free integer sum): one workgroup per hypothesis
+    // left 50 of 256 CUs streaming ~20K trajectories each at one wave per SIMD, latency-bound
+    const int S = std::max(1, std::min(16, N / 1024));
+    if (hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * (size_t)nhyp, s)) return e;
     if (precision == MDX_SUBSPACE_F32) {
         float* pbuf = reinterpret_cast<float*>(qbuf);
-        hipLaunchKernelGGL(k_subspace_hyp_f32, dim3(nhyp), dim3(256), 0, s, data, N, n, d, cols, inlier_thr, pbuf,
+        hipLaunchKernelGGL(k_subspace_hyp_f32, dim3(nhyp, S), dim3(256), 0, s, data, N, n, d, cols, inlier_thr, pbuf,
                            counts);
         hipLaunchKernelGGL(k_subspace_final_f32, dim3((N + 255) / 256), dim3(256), 0, s, data, N, n, nhyp, counts,
                            pbuf, out_thr, residuals, is_outlier, best);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(k_subspace_hyp, dim3(nhyp), dim3(256), 0, s, data, N, n, d, cols, inlier_thr, qbuf, counts);
+    hipLaunchKernelGGL(k_subspace_hyp, dim3(nhyp, S), dim3(256), 0, s, data, N, n, d, cols, inlier_thr, qbuf, counts);
     hipLaunchKernelGGL(k_subspace_final, dim3((N + 255) / 256), dim3(256), 0, s, data, N, n, d, nhyp, counts, qbuf,
                        out_thr, residuals, is_outlier, best);
     return hipGetLastError();
