@@ -55,12 +55,13 @@ struct mdx_ctx {
     DevBuf cls, Abuf, ctab;                  // LK v2: class planes, A sums, residue tables
     DevBuf dbg;                              // LK v2 per-level trace (MDX_LK_DEBUG=1)
     DevBuf csum;                             // classify: per-block summaries
-    DevBuf tin, tcur, tnp, tst, ttraj, tlen, tvec, tstart, tnum;   // trajectory tracking
+    DevBuf tin, tcur, tnp, tst, ttraj, tlen, tvec, tstart, tnum, tflag;   // trajectory tracking
     DevBuf straj, sdata, sq, scnt, scols, sres, sout, sbest;      // subspace RANSAC
     DevBuf ring_pyr, ring_der, rin;          // resident frame ring (mdx_ring_*)
     std::vector<int> ring_order;             // held slots, oldest first
     int ring_cap = 0, ring_w = 0, ring_h = 0, ring_ml = -1;
     bool lk_debug = false;
+    bool traj_chain = true;                  // trajectory passes in one launch (MDX_TRAJ_CHAIN=0: per pass)
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
     int lk_sub = 0;                          // > 0: LK sub-batch cap (MDX_LK_SUB, tests)
@@ -342,6 +343,7 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     if (const char* e = std::getenv("MDX_LK_G")) c->lk_g = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_SUB")) c->lk_sub = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
+    if (const char* e = std::getenv("MDX_TRAJ_CHAIN")) c->traj_chain = std::atoi(e) != 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         g_create_err = "hipStreamCreate failed";
         delete c;
@@ -390,7 +392,7 @@ extern "C" int mdx_destroy(mdx_ctx* c)
     DevBuf* bufs[] = {&c->pyr1, &c->pyr2, &c->der, &c->fits, &c->in1, &c->in2, &c->np, &c->st,
                       &c->vec, &c->mask, &c->H, &c->Hext, &c->num, &c->bnp, &c->bst,
                       &c->cls, &c->Abuf, &c->ctab, &c->dbg, &c->csum, &c->tin, &c->tcur, &c->tnp, &c->tst,
-                      &c->ttraj, &c->tlen, &c->tvec, &c->tstart, &c->tnum, &c->straj, &c->sdata, &c->sq,
+                      &c->ttraj, &c->tlen, &c->tvec, &c->tstart, &c->tnum, &c->tflag, &c->straj, &c->sdata, &c->sq,
                       &c->scnt, &c->scols, &c->sres, &c->sout, &c->sbest, &c->ring_pyr, &c->ring_der, &c->rin};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
@@ -815,8 +817,43 @@ static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int
     float* tr = c->ttraj.as<float>();
     int* tl = c->tlen.as<int>();
     int* dnum = c->tnum.as<int>();
-    HIP_OR_RETURN(c, launch_traj_init(s, npts, ny, P.pixel_step, nimg, cur, tr, tl, dnum));
-    for (int j = 0; j + 1 < nimg && npts > 0; j++) {
+    const bool chain = c->traj_chain && nimg <= kMaxTrajImgs && npts > 0;
+    if (chain && (rc = ensure(c, c->tflag, pts * 4)) != MDX_OK) return rc;
+    HIP_OR_RETURN(c, launch_traj_init(s, npts, ny, P.pixel_step, nimg, cur, tr, tl, dnum,
+                                      chain ? c->tflag.as<int>() : nullptr));
+    if (chain) {
+        // every pass in one launch: pass j + 1 of a point starts as soon as its pass j is done, so
+        // the passes' launch tails overlap (the per-pass launches below leave each tail idle)
+        LkArgs a{};
+        a.g = g;
+        a.maxl = g.nlev - 1;
+        a.npts = npts;
+        a.ny = ny;
+        a.nyg = ny;
+        a.pixel_step = P.pixel_step;
+        a.max_iters = std::min(std::max(P.max_iters, 0), 100);
+        a.min_eig = P.min_eig;
+        const double e = std::min(std::max(P.eps, 0.), 10.);
+        a.eps2 = e * e;
+        TrajChain t{};
+        for (int j = 0; j < nimg; j++) {
+            t.pyr[j] = pyr[j];
+            t.der[j] = der[j];
+        }
+        t.nimg = nimg;
+        t.w = w;
+        t.h = h;
+        t.cur = cur;
+        t.traj = tr;
+        t.tlen = tl;
+        t.flag = c->tflag.as<int>();
+        t.vectors = c->tvec.as<double>();
+        t.start_pts = c->tstart.as<float>();
+        t.num = dnum;
+        t.mvs = P.min_vector_size;
+        HIP_OR_RETURN(c, launch_lk_chain(s, a, t));
+    }
+    for (int j = 0; !chain && j + 1 < nimg && npts > 0; j++) {
         LkArgs a{};
         a.pyr1 = pyr[j];
         a.pyr2 = pyr[j + 1];

@@ -140,6 +140,25 @@ hipError_t launch_pyr_levels(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* p
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level,
                          int prow0 = 0, int prow1 = -1);
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);
+
+// Trajectory passes in one launch (k_lk chain mode): pass j of point p tracks frame j -> j+1 from
+// the point pass j-1 left, waiting for it through flag[p]; the pass bookkeeping of
+// calculateOpticalFlowTrajectory (k_traj_update's) is done by the point's own wave.
+constexpr int kMaxTrajImgs = 16;
+struct TrajChain {
+    const uint8_t* pyr[kMaxTrajImgs];    // padded pyramid slab of each frame
+    const uint32_t* der[kMaxTrajImgs];   // its Scharr planes
+    int nimg, w, h;
+    float* cur;                          // [npts][2] current points (atomic hand-off between passes)
+    float* traj;                         // [npts][nimg][2]
+    int* tlen;                           // [npts]
+    int* flag;                           // [npts] passes done (zeroed by k_traj_init)
+    double* vectors;                     // [npts][4] Vec4d of the last pass, or null
+    float* start_pts;                    // [npts][2] start points of the last pass, or null
+    int* num;                            // num_vectors
+    double mvs;                          // min_vector_size
+};
+hipError_t launch_lk_chain(hipStream_t s, const LkArgs& a, const TrajChain& t);
 // Trajectory subspace RANSAC (fitSubspace): mean-subtracted data, nhyp hypotheses of d columns
 // (cols: [nhyp][d]), winner's residuals / outlier flags; best[0] = winner or -1.  Scratch: data
 // [N][2T] floats + 2 (the means), qbuf [nhyp][2T][2T-d] doubles (MDX_SUBSPACE_F32: [nhyp][2T][2T] floats), counts [nhyp].
@@ -148,7 +167,7 @@ hipError_t launch_subspace(hipStream_t s, const float* traj, int N, int T, int d
                            uint8_t* is_outlier, int* best, int precision);
 // Trajectory tracking (calculateOpticalFlowTrajectory): grid init and the per-pass point update.
 hipError_t launch_traj_init(hipStream_t s, int npts, int ny, int pixel_step, int nimg, float* cur, float* traj,
-                            int* tlen, int* num);
+                            int* tlen, int* num, int* flag = nullptr);
 hipError_t launch_traj_update(hipStream_t s, int npts, const float* next_pts, const uint8_t* status, float* cur,
                               float* traj, int* tlen, int nimg, int w, int h, int last, double min_vector_size,
                               double* vectors, float* start_pts, int* num);

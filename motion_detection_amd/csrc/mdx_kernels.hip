@@ -468,8 +468,13 @@ __global__ __launch_bounds__(256) void k_scharr(const uint8_t* __restrict__ pyr1
 // order.  The result is bit-identical to the x86 reference, not merely within tolerance.
 typedef short s2k __attribute__((ext_vector_type(2)));
 
-template <int LPP>
-__global__ __launch_bounds__(64) void k_lk(LkArgs a)
+// k_lk<LPP, true>: the chained trajectory passes (TrajChain); grid = nimg-1 passes x npts points,
+// pass-major, one point per wave.
+constexpr int kChainSpinMax = 1 << 19;   // ~0.1 s of s_sleep(8) polls: a lost hand-off gives wrong
+                                         // results, never a hung launch
+
+template <int LPP, bool CHAIN>
+__global__ __launch_bounds__(64) void k_lk(LkArgs a, TrajChain t)
 {
     constexpr int WIN = 40, R = 8, NCH = WIN / R, EC = R * WIN / LPP, NE = NCH * EC, PPW = 64 / LPP;
     constexpr int STRIDE = 88;                 // floats per chain (80 used; 4*odd => b128 conflict-free)
@@ -478,10 +483,14 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a)
     constexpr float FLT_SCALE = 1.f / (1 << 20);
     __shared__ float4 lds4[PPW * PT_FLOATS / 4];
 
+    static_assert(!CHAIN || LPP == 64, "chain mode: one point per wave");
     const int lane = threadIdx.x;
     const int p = lane / LPP, s = lane % LPP;
-    const int pt = blockIdx.x * PPW + p;
-    const int pair = blockIdx.y;
+    // chain mode: block b = pass * npts + point (dispatch order: every block a wave waits for was
+    // dispatched before it, and pass 0 never waits, so the waits always drain)
+    const int pass = CHAIN ? (int)(blockIdx.x / (unsigned)a.npts) : 0;
+    const int pt = CHAIN ? (int)(blockIdx.x - (unsigned)pass * (unsigned)a.npts) : (int)blockIdx.x * PPW + p;
+    const int pair = CHAIN ? 0 : blockIdx.y;
     const bool valid = pt < a.npts;
     float* ch = reinterpret_cast<float*>(lds4) + p * PT_FLOATS;
     float* res = ch + 12 * STRIDE;
@@ -509,7 +518,23 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a)
 
     const int gx = valid ? pt / a.ny : 0, gy = valid ? pt % a.ny : 0;
     float px0 = (float)(gx * a.pixel_step), py0 = (float)(gy * a.pixel_step);
-    if (a.prev_pts && valid) {   // trajectory passes: arbitrary start points (flags 0: nextPt = prevPt)
+    if constexpr (CHAIN) {
+        // the point pass - 1 left (k_traj_init's grid point for pass 0): wait for that pass, then
+        // read it past the caches (the MI355X_MICROARCH.md hand-off: the writer stores sc1, waits
+        // vmcnt(0), then bumps the flag)
+        if (valid) {
+            if (pass > 0)
+                for (int n = 0; __hip_atomic_load(t.flag + pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pass &&
+                                n < kChainSpinMax;
+                     n++)
+                    __builtin_amdgcn_s_sleep(8);
+            const float2 c = __builtin_bit_cast(
+                float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(t.cur) + pt, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT));
+            px0 = c.x;
+            py0 = c.y;
+        }
+    } else if (a.prev_pts && valid) {   // trajectory passes: arbitrary start points (flags 0: nextPt = prevPt)
         const float* pp = a.prev_pts + ((long long)pair * a.npts + pt) * 2;
         px0 = pp[0];
         py0 = pp[1];
@@ -520,9 +545,9 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a)
     uint32_t sd[NE];              // (Ix & 0xffff) | Iy << 16
     uint32_t si[(NE + 1) / 2];    // I*32 values, two per word
 
-    const uint8_t* slab1 = a.pyr1 + (long long)pair * a.g.img_bytes;
-    const uint8_t* slab2 = a.pyr2 + (long long)pair * a.g.img_bytes;
-    const uint32_t* dslab = a.der + (long long)pair * a.g.der_words;
+    const uint8_t* slab1 = CHAIN ? t.pyr[pass] : a.pyr1 + (long long)pair * a.g.img_bytes;
+    const uint8_t* slab2 = CHAIN ? t.pyr[pass + 1] : a.pyr2 + (long long)pair * a.g.img_bytes;
+    const uint32_t* dslab = CHAIN ? t.der[pass] : a.der + (long long)pair * a.g.der_words;
 
     for (int level = a.maxl; level >= 0; --level) {
         const Level L = a.g.lv[level];
@@ -759,7 +784,42 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a)
         }
     }
 
-    if (valid && s == 0) {
+    if constexpr (CHAIN) {
+        // k_traj_update's bookkeeping for this point and pass (optical_flow_calculator.cpp:178-242)
+        if (valid && s == 0) {
+            const bool last = pass == t.nimg - 2;
+            double* v = (last && t.vectors) ? t.vectors + 4LL * pt : nullptr;
+            if (last && t.start_pts) {
+                t.start_pts[2 * pt] = px0;
+                t.start_pts[2 * pt + 1] = py0;
+            }
+            if (status) {
+                const float ex = npx, ey = npy;
+                if (last) {
+                    const float xd = ex - px0, yd = ey - py0;
+                    if (fabs((double)fabsf(xd)) > t.mvs || fabs((double)fabsf(yd)) > t.mvs) {
+                        if (v) { v[0] = px0; v[1] = py0; v[2] = xd; v[3] = yd; }
+                        atomicAdd(t.num, 1);
+                    } else if (v) {
+                        v[0] = px0; v[1] = py0; v[2] = 0.0; v[3] = 0.0;
+                    }
+                }
+                if (ex > 10.0f && ey > 10.0f && ex < (float)(t.w - 10) && ey < (float)(t.h - 10)) {
+                    __hip_atomic_store(reinterpret_cast<unsigned long long*>(t.cur) + pt,
+                                       __builtin_bit_cast(unsigned long long, make_float2(ex, ey)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    const int l = __hip_atomic_load(t.tlen + pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    t.traj[((long long)pt * t.nimg + l) * 2] = ex;
+                    t.traj[((long long)pt * t.nimg + l) * 2 + 1] = ey;
+                    __hip_atomic_store(t.tlen + pt, l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else if (v) {
+                v[0] = -1.0; v[1] = -1.0; v[2] = 0.0; v[3] = 0.0;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(t.flag + pt, pass + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else if (valid && s == 0) {
         const long long o = (long long)pair * a.npts + pt;
         a.next_pts[2 * o] = npx;
         a.next_pts[2 * o + 1] = npy;
@@ -1382,11 +1442,13 @@ hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t
 // OpticalFlowCalculator::calculateOpticalFlowTrajectory (optical_flow_calculator.cpp:133-257).
 // init: points = the grid (:148-158, x-major), every trajectory = its grid point.
 __global__ void k_traj_init(int npts, int ny, int pixel_step, int nimg, float* __restrict__ cur,
-                            float* __restrict__ traj, int* __restrict__ tlen, int* __restrict__ num)
+                            float* __restrict__ traj, int* __restrict__ tlen, int* __restrict__ num,
+                            int* __restrict__ flag)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) *num = 0;
     if (i >= npts) return;
+    if (flag) flag[i] = 0;
     const float x = (float)((i / ny) * pixel_step), y = (float)((i % ny) * pixel_step);
     cur[2 * i] = x;
     cur[2 * i + 1] = y;
@@ -1436,10 +1498,18 @@ __global__ void k_traj_update(int npts, const float* __restrict__ next_pts, cons
 }
 
 hipError_t launch_traj_init(hipStream_t s, int npts, int ny, int pixel_step, int nimg, float* cur, float* traj,
-                            int* tlen, int* num)
+                            int* tlen, int* num, int* flag)
 {
     hipLaunchKernelGGL(k_traj_init, dim3((npts + 255) / 256 > 0 ? (npts + 255) / 256 : 1), dim3(256), 0, s, npts, ny,
-                       pixel_step, nimg, cur, traj, tlen, num);
+                       pixel_step, nimg, cur, traj, tlen, num, flag);
+    return hipGetLastError();
+}
+
+hipError_t launch_lk_chain(hipStream_t s, const LkArgs& a, const TrajChain& t)
+{
+    const long long blocks = (long long)(t.nimg - 1) * a.npts;
+    if (t.nimg < 2 || t.nimg > kMaxTrajImgs || a.npts <= 0 || blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_lk<64, true>), dim3((unsigned)blocks), dim3(64), 0, s, a, t);
     return hipGetLastError();
 }
 
@@ -1459,7 +1529,7 @@ hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a)
     // per SIMD, and ran the trajectory passes 1.5x slower)
     constexpr int LPP = 64, PPW = 64 / LPP;
     const dim3 grid((a.npts + PPW - 1) / PPW, batch);
-    hipLaunchKernelGGL(k_lk<LPP>, grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL((k_lk<LPP, false>), grid, dim3(64), 0, s, a, TrajChain{});
     return hipGetLastError();
 }
 
