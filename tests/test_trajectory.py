@@ -111,6 +111,9 @@ GPU_CASES = [
     (640, 480, 3, 7, 1, 3),
     (200, 150, 2, 5, 1, 4),
     (1280, 720, 5, 10, 3, 5),
+    # the chained launch at its frame limit (16), and past it (the per-pass launches)
+    (200, 150, 16, 10, 1, 6),
+    (160, 120, 18, 9, 1, 7),
 ]
 
 
@@ -171,3 +174,25 @@ def test_trajectory_flat_and_two_frames(mdx, ctx, oracle):
     ref = oracle.flow_trajectory(frames, pixel_step=10)
     _compare(res, ref, "flat")
     assert res.num_vectors == 0
+
+
+@pytest.mark.gpu
+def test_trajectory_chain_equals_per_pass_launches(mdx, oracle, monkeypatch):
+    """The chained launch (all passes in one k_lk launch, per-point hand-off) and the per-pass
+    launches (MDX_TRAJ_CHAIN=0, read at context creation) give the same bits."""
+    w, h, n = 480, 360, 6
+    frames = sequence(mdx, oracle, w, h, n, seed=12, channels=3)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MDX_TRAJ_CHAIN", mode)
+        c = mdx.Context(0, w, h, 1)
+        try:
+            out[mode] = c.flow_trajectory(frames)
+        finally:
+            c.close()
+    a, b = out["1"], out["0"]
+    assert a.num_vectors == b.num_vectors
+    np.testing.assert_array_equal(a.traj_len, b.traj_len)
+    np.testing.assert_array_equal(a.traj.view(np.uint32), b.traj.view(np.uint32))
+    np.testing.assert_array_equal(a.start_pts.view(np.uint32), b.start_pts.view(np.uint32))
+    np.testing.assert_array_equal(a.vectors.view(np.uint64), b.vectors.view(np.uint64))
