@@ -811,7 +811,7 @@ static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int
     if ((rc = ensure(c, c->tlen, pts * 4)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->tvec, pts * 32)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->tstart, pts * 8)) != MDX_OK) return rc;
-    if ((rc = ensure(c, c->tnum, 4)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->tnum, 8)) != MDX_OK) return rc;
     hipStream_t s = c->stream;
     float* cur = c->tcur.as<float>();
     float* tr = c->ttraj.as<float>();
@@ -883,8 +883,12 @@ static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int
         if (start_pts) HIP_OR_RETURN(c, hipMemcpyAsync(start_pts, c->tstart.p, (size_t)npts * 8, hipMemcpyDeviceToHost, s));
         if (vectors) HIP_OR_RETURN(c, hipMemcpyAsync(vectors, c->tvec.p, (size_t)npts * 32, hipMemcpyDeviceToHost, s));
     }
-    HIP_OR_RETURN(c, hipMemcpyAsync(&num, dnum, 4, hipMemcpyDeviceToHost, s));
+    int counts[2] = {0, 0};
+    HIP_OR_RETURN(c, hipMemcpyAsync(counts, dnum, chain ? 8 : 4, hipMemcpyDeviceToHost, s));
     HIP_OR_RETURN(c, hipStreamSynchronize(s));
+    num = counts[0];
+    if (chain && counts[1] != 0)
+        return set_err(c, MDX_EHIP, "trajectory passes: %d point hand-off(s) timed out", counts[1]);
     if (num_vectors) *num_vectors = num;
     return MDX_OK;
 }

@@ -155,7 +155,7 @@ struct TrajChain {
     int* flag;                           // [npts] passes done (zeroed by k_traj_init)
     double* vectors;                     // [npts][4] Vec4d of the last pass, or null
     float* start_pts;                    // [npts][2] start points of the last pass, or null
-    int* num;                            // num_vectors
+    int* num;                            // [0] num_vectors, [1] hand-off waits that timed out
     double mvs;                          // min_vector_size
 };
 hipError_t launch_lk_chain(hipStream_t s, const LkArgs& a, const TrajChain& t);

@@ -523,11 +523,15 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a, TrajChain t)
         // read it past the caches (the MI355X_MICROARCH.md hand-off: the writer stores sc1, waits
         // vmcnt(0), then bumps the flag)
         if (valid) {
-            if (pass > 0)
-                for (int n = 0; __hip_atomic_load(t.flag + pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pass &&
-                                n < kChainSpinMax;
-                     n++)
+            if (pass > 0) {
+                int n = 0;
+                while (__hip_atomic_load(t.flag + pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pass &&
+                       n < kChainSpinMax) {
                     __builtin_amdgcn_s_sleep(8);
+                    n++;
+                }
+                if (n >= kChainSpinMax && s == 0) atomicAdd(t.num + 1, 1);   // reported as an error by the host
+            }
             const float2 c = __builtin_bit_cast(
                 float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(t.cur) + pt, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT));
@@ -1446,7 +1450,10 @@ __global__ void k_traj_init(int npts, int ny, int pixel_step, int nimg, float* _
                             int* __restrict__ flag)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) *num = 0;
+    if (i == 0) {
+        num[0] = 0;
+        if (flag) num[1] = 0;   // chain mode: hand-off timeouts
+    }
     if (i >= npts) return;
     if (flag) flag[i] = 0;
     const float x = (float)((i / ny) * pixel_step), y = (float)((i % ny) * pixel_step);
