@@ -156,6 +156,35 @@ def cpu_baseline(uniq, w, h, seconds: float, threads: int):
                        f"the OpenCV 2.4 path, {threads} thread(s) over LK points / warp rows), {el:.1f} s wall")
 
 
+def check_outputs(uniq, outs, B, w, h, ps, threads):
+    """Untimed checker (test infrastructure, like cpu_baseline): the oracle's results for the
+    `unique` distinct pairs, compared bit for bit with every one of the B slots of the last timed
+    step (slot i holds pair i % unique): next_pts (float32 bits), status, H (float64 bits), mask and
+    num_vectors.  Returns the counts; a mismatch is reported in the line, never hidden."""
+    from oracle import pyoracle
+    pyoracle.build()
+    refs = [pyoracle.calculate_optical_flow(a, b, nthreads=threads, pixel_step=ps, min_vector_size=1.0)
+            for a, b, _ in uniq]
+    bad = []
+    for i in range(B):
+        r = refs[i % len(refs)]
+        diffs = []
+        if int(outs["num"][i]) != r["num_vectors"]:
+            diffs.append("num_vectors")
+        if not np.array_equal(outs["st"][i], r["status"]):
+            diffs.append("status")
+        if not np.array_equal(outs["np"][i].view(np.uint32), r["next_pts"].view(np.uint32)):
+            diffs.append("next_pts")
+        if not np.array_equal(outs["H"][i].view(np.uint64), r["H"].ravel().view(np.uint64)):
+            diffs.append("H")
+        if not np.array_equal(outs["mask"][i], r["mask"]):
+            diffs.append("mask")
+        if diffs:
+            bad.append({"slot": i, "differs": diffs})
+    return dict(checked_pairs=B, distinct_pairs=len(refs), mismatched_pairs=len(bad), mismatches=bad[:8],
+                compared="next_pts bits, status, H bits, mask, num_vectors vs oracle/ (untimed)")
+
+
 REHEARSE = False   # --rehearse: ranks beyond the visible devices may share device 0
 
 
@@ -500,6 +529,8 @@ def main():
                     help="allow more ranks than visible GPUs (they share device 0; n_gpus counts distinct devices)")
     ap.add_argument("--no-lk-roofline", action="store_true", help="skip the LK iteration census (profiling runs)")
     ap.add_argument("--probe-ranks", action="store_true", help="launch plumbing only: ranks report over gloo, no GPU")
+    ap.add_argument("--no-pipelining", action="store_true", help="time the main leg with call pipelining off")
+    ap.add_argument("--no-parity", action="store_true", help="skip the untimed oracle check of the last step")
     args = ap.parse_args()
     global REHEARSE
     REHEARSE = args.rehearse
@@ -515,11 +546,12 @@ def main():
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
     if args.workload == "c4":
         return main_c4(args, D, threads)
-    # Call pipelining: a device-entry call's front end may start beside the previous
-    # call's last LK level and fit/warp.  Its contract -- inputs already in HBM when the call is made
-    # -- holds here (the synthetic pairs are uploaded once, before the timed steps).  MDX_PIPE=0 turns
-    # it off; C4's band calls measured 3% slower with it, so that workload leaves it off.
-    os.environ.setdefault("MDX_PIPE", "1")
+    # Call pipelining (mdx_params.call_pipelining): a device-entry call's front end may
+    # start beside the previous call's last LK level and fit/warp.  Its contract -- inputs already in
+    # HBM when the call is made -- holds here (the synthetic pairs are uploaded once, before the timed
+    # steps).  The line also reports the rate without it (value_unpipelined).  C4's band calls measured
+    # 3% slower with it, so that workload leaves it off.
+    pipe = 0 if args.no_pipelining else 1
     w, h = CONFIGS[args.config]
     B = args.batch or {"640": 128, "1080p": 32, "4k": 8, "8k": 2}[args.config]
     unique = max(1, min(args.unique, B))
@@ -529,40 +561,61 @@ def main():
                                   SEED0 + 1000 * D.rank, threads)
     if args.only_roofline:
         B, unique = 1, 1
-    ctx = open_ctx(D, w, h, B, pixel_step=ps, min_vector_size=1.0)
+    ctx = open_ctx(D, w, h, B, pixel_step=ps, min_vector_size=1.0, call_pipelining=pipe)
     devs = gather_devices(D, ctx)
+    n = mdx.grid_count(w, h, ps)
     d1, d2 = ctx.dev_alloc(g1.nbytes), ctx.dev_alloc(g2.nbytes)
-    dmask = ctx.dev_alloc(B * w * h)
-    dnum = ctx.dev_alloc(B * 4)
+    dout = {k: ctx.dev_alloc(sz) for k, sz in dict(np=B * n * 8, st=B * n, mask=B * w * h, H=B * 72,
+                                                      num=B * 4).items()}
     ctx.h2d(d1, g1)
     ctx.h2d(d2, g2)
 
     def step():
-        ctx.flow_warp_diff_batch_dev(B, d1, d2, w, h, w, w * h, mdx.FMT_GRAY8, d_mask=dmask, d_num_vectors=dnum)
+        ctx.flow_warp_diff_batch_dev(B, d1, d2, w, h, w, w * h, mdx.FMT_GRAY8, d_next_pts=dout["np"],
+                                     d_status=dout["st"], d_mask=dout["mask"], d_H=dout["H"],
+                                     d_num_vectors=dout["num"])
+
+    def timed(k):
+        """k steps between barriers + device syncs (the device sync also reports an LK hand-off
+        timeout as an error); returns this rank's wall seconds."""
+        D.barrier()
+        ctx.device_sync()
+        t = time.perf_counter()
+        for _ in range(k):
+            step()
+        ctx.device_sync()
+        D.barrier()
+        return time.perf_counter() - t
 
     full_steps = 1 if args.only_roofline else args.steps
     for _ in range(0 if args.only_roofline else args.warmup):
         step()
     ctx.device_sync()
-    num = np.empty(B, np.int32)
-    ctx.d2h(num, dnum)
 
     ctx.enable_timing(True)
-    D.barrier()
-    ctx.device_sync()
-    t0 = time.perf_counter()
-    for _ in range(full_steps):
-        step()
-    ctx.device_sync()
-    D.barrier()
-    el = time.perf_counter() - t0
+    el = timed(full_steps)
     px_rate, el_max = throughput(D, float(full_steps * B * w * h), el)
     value = px_rate / 1e6
     px_all = px_rate * el_max
     st = ctx.stage_ms()
     calls = max(st["calls"], 1)
     stages = {k: round(v / calls, 4) for k, v in st.items() if k != "calls"}
-    for p in (d1, d2, dmask, dnum):
+    # the last timed step's outputs, checked against the oracle after every timed leg (untimed)
+    outs = {k: np.empty(shape, dt) for k, shape, dt in (("np", (B, n, 2), np.float32), ("st", (B, n), np.uint8),
+                                                         ("mask", (B, h, w), np.uint8), ("H", (B, 9), np.float64),
+                                                         ("num", (B,), np.int32))}
+    for k, arr in outs.items():
+        ctx.d2h(arr, dout[k])
+    num = outs["num"]
+    # the same steps with call pipelining off (the line's value_unpipelined)
+    value_unpiped = None
+    if pipe and not args.only_roofline:
+        ctx.set_params(call_pipelining=0)
+        step()
+        el_u = timed(full_steps)
+        value_unpiped = round(throughput(D, float(full_steps * B * w * h), el_u)[0] / 1e6, 2)
+        ctx.set_params(call_pipelining=1)
+    for p in [d1, d2] + list(dout.values()):
         ctx.dev_free(p)
     del g1, g2
 
@@ -572,7 +625,7 @@ def main():
         kw, kh = CONFIGS["4k"]
         KB = 8
         k1, k2, _, _ = make_batch(kw, kh, KB, min(4, KB), SEED0 + 500 + 1000 * D.rank, threads)
-        kctx = open_ctx(D, kw, kh, KB, pixel_step=ps, min_vector_size=1.0)
+        kctx = open_ctx(D, kw, kh, KB, pixel_step=ps, min_vector_size=1.0, call_pipelining=pipe)
         f1, f2, fm = kctx.dev_alloc(k1.nbytes), kctx.dev_alloc(k2.nbytes), kctx.dev_alloc(KB * kw * kh)
         kctx.h2d(f1, k1); kctx.h2d(f2, k2)
 
@@ -630,6 +683,9 @@ def main():
         rctx.close()
         del r1, r2
 
+    parity = None
+    if not args.only_roofline and not args.no_parity:
+        parity = check_outputs(uniq, outs, B, w, h, ps, host_cores()["available"])
     cpu = cpu1 = None
     if D.world == 1 and not args.no_cpu:
         hc = host_cores()
@@ -673,8 +729,11 @@ def main():
         "config": {"workload": f"{w}x{h} gray frame pairs through the full reference path (pyramid + Scharr, "
                                f"pyramidal LK 40x40 / 10 iters, first-4 perspective fit, warp+absdiff+threshold)",
                    "frame": f"{w}x{h}", "pixel_step": ps, "grid_points_per_pair": mdx.grid_count(w, h, ps),
-                   "batch_per_gpu": B, "unique_pairs_per_gpu": unique,
+                   "batch_per_gpu": B, "unique_pairs_per_gpu": unique, "call_pipelining": bool(pipe),
                    "parallelism": f"{D.world} independent stream shard(s), one per GPU, no collectives"},
+        "value_unpipelined": value_unpiped,
+        "parity_checked_pairs": parity["checked_pairs"] if parity else 0,
+        "parity": parity,
         "roofline": roof,
         "cpu_baseline": cpu,
         "cpu_baseline_1core": cpu1,

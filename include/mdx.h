@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define MDX_ABI_VERSION 1
+#define MDX_ABI_VERSION 2    /* 2: mdx_params.call_pipelining, mdx_input_ready */
 
 /* Return codes */
 #define MDX_OK           0
@@ -62,7 +62,19 @@ typedef struct {
     double min_vector_size;  /* ROS param min_vector_size, default 1.0 (node.cpp:44) */
     int    fit_mode;         /* MDX_FIT_FIRST4 (default) or MDX_FIT_EXTERNAL */
     int    subspace_precision; /* mdx_fit_subspace arithmetic: MDX_SUBSPACE_F64 (default) or _F32 */
+    int    call_pipelining;  /* 0 (default) or 1: consecutive device-entry calls overlap (below) */
 } mdx_params;
+
+/*
+ * Call pipelining (mdx_params.call_pipelining = 1).  The pyramid workspace holds two halves used by
+ * alternate device-entry calls (mdx_flow_warp_diff_batch_dev, mdx_band_flow_dev), and a call's
+ * front end (gray, pyramids) runs on the context's second stream, behind the previous call's
+ * flow-independent LK work, so it overlaps that call's last LK level and its fit/warp.  The front
+ * end then does NOT wait for earlier work on the context stream: the call's input frames must be
+ * in HBM when it is made (mdx_memcpy_h2d returns after the copy), or the caller names the event
+ * after which they are, with mdx_input_ready.  Outputs are unaffected; results are identical with
+ * and without pipelining.  The workspace doubles its pyramid slabs while the flag is set.
+ */
 
 typedef struct mdx_ctx mdx_ctx;
 
@@ -92,9 +104,19 @@ int mdx_device_pci(const mdx_ctx* ctx, char* buf, int len);
 /* Build provenance: "src_sha256=<sha256 of the library's sources> arch=gfx950", compiled in by
  * csrc/Makefile.  tests/test_abi.py checks it against the sources in the tree. */
 const char* mdx_build_info(void);
+/* Wait for the context's work.  Returns MDX_EHIP if an LK hand-off between pyramid levels timed
+ * out in any call since the last check (the LK level dataflow of the batched entry: a group waits,
+ * bounded, for its pair's coarser level); the outputs of those calls are then invalid.  A wait
+ * that long means the device was preempted or oversubscribed; it is never silent. */
 int mdx_sync(mdx_ctx* ctx);
-/* hipDeviceSynchronize on the context's device (all streams). */
+/* hipDeviceSynchronize on the context's device (all streams); the same hand-off check. */
 int mdx_device_sync(mdx_ctx* ctx);
+/* Name the input frames' producer: the next device-entry call (mdx_flow_warp_diff_batch_dev,
+ * mdx_band_flow_dev, mdx_warp_diff_dev) makes its first stage wait for `hip_event` (a hipEvent_t
+ * the caller recorded on its own stream after writing the frames) before reading them.  One-shot:
+ * consumed by that call.  Needed with call pipelining whenever the frames are produced
+ * asynchronously (a zero-copy producer on another stream); harmless without it. */
+int mdx_input_ready(mdx_ctx* ctx, void* hip_event);
 
 /*
  * Synchronous host-buffer entry: the direct replacement of calculateOpticalFlow.
@@ -163,8 +185,10 @@ int mdx_warp_diff_dev(mdx_ctx* ctx, int batch, const uint8_t* d_gray1, const uin
  * Both entries are asynchronous on the context stream.  Step 3 reads the pyramids of the
  * context's latest mdx_band_flow_dev call, which must be of the same frame pair (several bands of
  * one pair may run step 1 one after another first), and converts from that call's d_img1 the
- * frame-1 rows its warp reads beyond the band, so d_img1 must still hold frame 1.  fit_mode must
- * be MDX_FIT_FIRST4.
+ * frame-1 rows its warp reads beyond the band, so d_img1 must still hold frame 1.  Any other entry
+ * that rebuilds the context's pyramids in between (a pair or trajectory call) voids them: step 3
+ * then returns MDX_EINVAL instead of warping another pair's frames.  fit_mode must be
+ * MDX_FIT_FIRST4.
  */
 typedef struct mdx_band_cand {
     int32_t count;     /* accepted vectors (status && |d| > min_vector_size) in the band */

@@ -36,7 +36,7 @@ EXPORTED = [
     "mdx_dev_free", "mdx_memcpy_h2d", "mdx_memcpy_d2h", "mdx_enable_timing", "mdx_timing_calls", "mdx_stage_ms",
     "mdx_synth_pair", "mdx_debug_copy", "mdx_band_flow_dev", "mdx_band_fit_warp_dev", "mdx_flow_trajectory",
     "mdx_srand", "mdx_rand", "mdx_fit_subspace", "mdx_device_pci", "mdx_build_info",
-    "mdx_ring_push", "mdx_ring_trajectory", "mdx_ring_reset",
+    "mdx_ring_push", "mdx_ring_trajectory", "mdx_ring_reset", "mdx_input_ready",
 ]
 
 # csrc/Makefile STAMPED: the files whose bytes the library's provenance stamp hashes, in order
@@ -62,7 +62,8 @@ assert C.sizeof(MdxBandCand) == BAND_CAND_BYTES
 class MdxParams(C.Structure):
     _fields_ = [("win", C.c_int), ("max_level", C.c_int), ("max_iters", C.c_int), ("eps", C.c_double),
                 ("min_eig", C.c_float), ("thresh", C.c_int), ("pixel_step", C.c_int),
-                ("min_vector_size", C.c_double), ("fit_mode", C.c_int), ("subspace_precision", C.c_int)]
+                ("min_vector_size", C.c_double), ("fit_mode", C.c_int), ("subspace_precision", C.c_int),
+                ("call_pipelining", C.c_int)]
 
 
 class MdxError(RuntimeError):
@@ -135,6 +136,8 @@ def lib() -> C.CDLL:
     L.mdx_build_info.restype = C.c_char_p
     L.mdx_device_sync.argtypes = [vp]
     L.mdx_device_sync.restype = C.c_int
+    L.mdx_input_ready.argtypes = [vp, vp]
+    L.mdx_input_ready.restype = C.c_int
     L.mdx_flow_warp_diff.argtypes = [vp, u8p, u8p, C.c_int, C.c_int, C.c_int, C.c_int, f32p, u8p, f64p, u8p,
                                      f64p, f64p, C.POINTER(C.c_int)]
     L.mdx_flow_warp_diff.restype = C.c_int

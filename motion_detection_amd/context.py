@@ -233,6 +233,11 @@ class Context:
         return self._check(lib().mdx_band_fit_warp_dev(self._h, nrec, v(d_cands), y0, y1, v(d_mask_band), v(d_H),
                                                        v(d_num_vectors)))
 
+    def input_ready(self, hip_event: int):
+        """The next device-entry call waits for this hipEvent_t (an int handle) before reading its
+        input frames (include/mdx.h mdx_input_ready; one-shot)."""
+        self._check(lib().mdx_input_ready(self._h, C.c_void_p(hip_event) if hip_event else None))
+
     def sync(self):
         self._check(lib().mdx_sync(self._h))
 

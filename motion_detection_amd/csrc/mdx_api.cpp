@@ -31,22 +31,31 @@ struct mdx_ctx {
     hipEvent_t lkev[kMaxLevels + 2] = {};    // launch_lk_v2's + the first frames' pyramids ready
     hipStream_t iter2 = nullptr;             // LK dataflow: every other level's iteration launch (MDX_LK_FLOW)
     hipEvent_t flowev[2] = {};
-    // Call pipelining (MDX_PIPE=1): the pyramid slabs have two halves used by alternate calls, and a
-    // call's front end runs on the aux stream right behind the previous call's last class planes
-    // and A sums, so it overlaps that call's last LK level and fit/warp.  (A stream of its own
-    // measured 1.9x slower: a process gets 4 hardware queues, and a fifth stream shares one, so
-    // its event waits block the work queued behind them.)
-    bool pipe = false;
+    // Call pipelining (mdx_params.call_pipelining): the pyramid slabs have two halves used by
+    // alternate calls, and a call's front end runs on the aux stream right behind the previous
+    // call's last class planes and A sums, so it overlaps that call's last LK level and fit/warp.
+    // (A stream of its own measured 1.9x slower: a process gets 4 hardware queues, and a fifth
+    // stream shares one, so its event waits block the work queued behind them.)
     hipEvent_t front_ev = nullptr;
     hipEvent_t pyr_free[2] = {};             // on `stream`, after the last reader of each half
     hipEvent_t lvl_done[kMaxLevels] = {};    // the last call's iteration launch of each level
     int pyr_half = 0;                        // the half the next pipelined call writes
-    int last_half = 0;
-    uint8_t* last_pyr1 = nullptr;            // the last pair call's pyramids (band fit/warp, debug copies)
+    hipEvent_t input_ev = nullptr;           // mdx_input_ready: the next device call's inputs (caller-owned)
+    uint8_t* last_pyr1 = nullptr;            // the last pair call's pyramids (debug copies)
     uint8_t* last_pyr2 = nullptr;
+    // the latest mdx_band_flow_dev's pyramids, which its fit/warp reads (band_w == 0: none, or
+    // voided by another call that rebuilt the slabs since)
+    uint8_t* band_pyr1 = nullptr;
+    uint8_t* band_pyr2 = nullptr;
+    int band_half = 0;
     const uint8_t* band_img1 = nullptr;      // the last mdx_band_flow_dev's frame 1 (its fit/warp reads it)
     int band_built[2] = {0, 0};              // level-0 rows of frame 1 that call's pyramid build wrote
     int band_stride = 0, band_fmt = 0;
+    // LK dataflow hand-off timeouts ([0] group waits, [1] gate waits), read back at the sync points
+    DevBuf errw;
+    int* err_host = nullptr;                 // pinned readback
+    int spin_max = kLkSpinDefault;           // MDX_LK_SPIN_MAX (debug: < 0 injects timeouts)
+    int lk_cap = 85;                         // MDX_LK_CAP: dataflow launch share of the resident waves (%)
     mdx_params prm{};
     int max_w = 0, max_h = 0, max_batch = 0;
     DevBuf pyr1, pyr2, der, fits;            // pyramid / derivative / fit workspace
@@ -108,6 +117,7 @@ extern "C" void mdx_default_params(mdx_params* p)
     p->min_vector_size = 1.0;
     p->fit_mode = MDX_FIT_FIRST4;
     p->subspace_precision = MDX_SUBSPACE_F64;
+    p->call_pipelining = 0;
 }
 
 extern "C" int mdx_grid_count(int w, int h, int ps)
@@ -126,6 +136,7 @@ static int check_params(const mdx_params* p, std::string* why)
         *why = "bad subspace_precision";
         return 0;
     }
+    if (p->call_pipelining != 0 && p->call_pipelining != 1) { *why = "call_pipelining must be 0 or 1"; return 0; }
     return 1;
 }
 
@@ -174,15 +185,16 @@ static int ensure(mdx_ctx* c, DevBuf& b, size_t need)
     return MDX_OK;
 }
 
-// Pyramid slabs hold two halves (call pipelining); non-pipelined users take the slab from its start.
+// With call pipelining the pyramid slabs hold two halves (ensure_workspace(.., two = true) makes the
+// slab at least twice one call's pyramids); other users take the slab from its start.
 static size_t pyr_half_bytes(const DevBuf& b) { return b.cap / 2 / 256 * 256; }
 
-static int ensure_workspace(mdx_ctx* c, const Geometry& g, int batch)
+static int ensure_workspace(mdx_ctx* c, const Geometry& g, int batch, bool two)
 {
     int rc;
     const size_t half = ((size_t)g.img_bytes * batch + 255) / 256 * 256;
-    if ((rc = ensure(c, c->pyr1, 2 * half)) != MDX_OK) return rc;
-    if ((rc = ensure(c, c->pyr2, 2 * half)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->pyr1, two ? 2 * half : half)) != MDX_OK) return rc;
+    if ((rc = ensure(c, c->pyr2, two ? 2 * half : half)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->der, (size_t)g.der_words * 4 * batch)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->fits, sizeof(PairFit) * (size_t)batch)) != MDX_OK) return rc;
     return MDX_OK;
@@ -359,24 +371,27 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
             ok = hipStreamCreateWithFlags(&c->iter2, hipStreamNonBlocking) == hipSuccess;
             for (int i = 0; ok && i < 2; i++) ok = hipEventCreateWithFlags(&c->flowev[i], hipEventDisableTiming) == hipSuccess;
         }
-        // opt-in: a pipelined device-entry call's front end does not wait for earlier work on the
-        // context stream, so its inputs must already be in HBM when the call is made
-        const char* ep = std::getenv("MDX_PIPE");
-        if (ok && ep && std::atoi(ep) != 0) {
-            c->pipe = true;
-            ok = hipEventCreateWithFlags(&c->front_ev, hipEventDisableTiming) == hipSuccess;
-            for (int i = 0; ok && i < 2; i++) ok = hipEventCreateWithFlags(&c->pyr_free[i], hipEventDisableTiming) == hipSuccess;
-            for (int i = 0; ok && i < kMaxLevels; i++)
-                ok = hipEventCreateWithFlags(&c->lvl_done[i], hipEventDisableTiming) == hipSuccess;
-        }
+        // call pipelining's events (mdx_params.call_pipelining may be switched on at any call)
+        ok = ok && hipEventCreateWithFlags(&c->front_ev, hipEventDisableTiming) == hipSuccess;
+        for (int i = 0; ok && i < 2; i++) ok = hipEventCreateWithFlags(&c->pyr_free[i], hipEventDisableTiming) == hipSuccess;
+        for (int i = 0; ok && i < kMaxLevels; i++)
+            ok = hipEventCreateWithFlags(&c->lvl_done[i], hipEventDisableTiming) == hipSuccess;
         if (!ok) {
             g_create_err = "aux stream / event creation failed";
             mdx_destroy(c);
             return nullptr;
         }
     }
+    if (const char* e = std::getenv("MDX_LK_CAP")) c->lk_cap = std::min(std::max(std::atoi(e), 10), 100);
+    if (const char* e = std::getenv("MDX_LK_SPIN_MAX")) c->spin_max = std::atoi(e);
+    if (ensure(c, c->errw, 16) != MDX_OK || hipMemset(c->errw.p, 0, 16) != hipSuccess ||
+        hipHostMalloc((void**)&c->err_host, 16, hipHostMallocDefault) != hipSuccess) {
+        g_create_err = "error-word allocation failed";
+        mdx_destroy(c);
+        return nullptr;
+    }
     Geometry g = make_geometry(max_w, max_h, prm.max_level);
-    if (ensure_workspace(c, g, max_batch) != MDX_OK) {
+    if (ensure_workspace(c, g, max_batch, prm.call_pipelining != 0) != MDX_OK) {
         g_create_err = c->err;
         mdx_destroy(c);
         return nullptr;
@@ -393,9 +408,11 @@ extern "C" int mdx_destroy(mdx_ctx* c)
                       &c->vec, &c->mask, &c->H, &c->Hext, &c->num, &c->bnp, &c->bst,
                       &c->cls, &c->Abuf, &c->ctab, &c->dbg, &c->csum, &c->tin, &c->tcur, &c->tnp, &c->tst,
                       &c->ttraj, &c->tlen, &c->tvec, &c->tstart, &c->tnum, &c->tflag, &c->straj, &c->sdata, &c->sq,
-                      &c->scnt, &c->scols, &c->sres, &c->sout, &c->sbest, &c->ring_pyr, &c->ring_der, &c->rin};
+                      &c->scnt, &c->scols, &c->sres, &c->sout, &c->sbest, &c->ring_pyr, &c->ring_der, &c->rin,
+                      &c->errw};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
+    if (c->err_host) (void)hipHostFree(c->err_host);
     if (c->ev) {
         for (int i = 0; i < mdx_ctx::kSlots * 7; i++) (void)hipEventDestroy(c->ev[i]);
         delete[] c->ev;
@@ -441,18 +458,62 @@ extern "C" int mdx_get_params(const mdx_ctx* c, mdx_params* p)
     return MDX_OK;
 }
 
+// The LK dataflow's hand-off timeouts since the last check: queue the error word's readback on the
+// context stream (every LK launch of a call is joined into it), and after the caller's sync
+// lk_err_result turns a nonzero count into MDX_EHIP and clears the word.
+static int queue_lk_err(mdx_ctx* c)
+{
+    HIP_OR_RETURN(c, hipMemcpyAsync(c->err_host, c->errw.p, 8, hipMemcpyDeviceToHost, c->stream));
+    return MDX_OK;
+}
+
+static int lk_err_result(mdx_ctx* c)
+{
+    const int groups = c->err_host[0], gates = c->err_host[1];
+    if (groups == 0 && gates == 0) return MDX_OK;
+    c->err_host[0] = c->err_host[1] = 0;
+    HIP_OR_RETURN(c, hipMemsetAsync(c->errw.p, 0, 8, c->stream));
+    HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
+    return set_err(c, MDX_EHIP,
+                   "LK level dataflow: %d group hand-off wait(s) and %d gate wait(s) timed out (device preempted or "
+                   "oversubscribed?); the outputs of the calls since the last sync are invalid",
+                   groups, gates);
+}
+
 extern "C" int mdx_sync(mdx_ctx* c)
 {
     if (!c) return MDX_EINVAL;
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    int rc = queue_lk_err(c);
+    if (rc != MDX_OK) return rc;
     HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
-    return MDX_OK;
+    return lk_err_result(c);
 }
 
 extern "C" int mdx_device_sync(mdx_ctx* c)
 {
     if (!c) return MDX_EINVAL;
     HIP_OR_RETURN(c, hipSetDevice(c->device));
+    int rc = queue_lk_err(c);
+    if (rc != MDX_OK) return rc;
     HIP_OR_RETURN(c, hipDeviceSynchronize());
+    return lk_err_result(c);
+}
+
+extern "C" int mdx_input_ready(mdx_ctx* c, void* hip_event)
+{
+    if (!c) return MDX_EINVAL;
+    c->input_ev = static_cast<hipEvent_t>(hip_event);
+    return MDX_OK;
+}
+
+// The next device call's first stage waits for the caller's input event (mdx_input_ready), once.
+static int wait_input(mdx_ctx* c, hipStream_t st)
+{
+    if (!c->input_ev) return MDX_OK;
+    hipEvent_t e = c->input_ev;
+    c->input_ev = nullptr;
+    HIP_OR_RETURN(c, hipStreamWaitEvent(st, e, 0));
     return MDX_OK;
 }
 
@@ -534,6 +595,9 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
     }
     a.plan = c->plan;
     a.max_sub = c->lk_sub;
+    a.err = c->errw.as<int>();
+    a.spin_max = c->spin_max;
+    a.flow_cap = c->lk_cap;
     a.cmap = c->ctab.as<int16_t>();
     a.rlist = c->ctab.as<int16_t>() + kMaxLevels * 2 * 128;
     a.ord = c->ctab.as<int16_t>() + 2 * kMaxLevels * 2 * 128;
@@ -554,7 +618,7 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
     HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
                                   reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes), prev_ready, c->iter2,
                                   c->flowev, reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes + qbytes),
-                                  c->pipe ? c->lvl_done : nullptr));
+                                  c->prm.call_pipelining ? c->lvl_done : nullptr));
     return MDX_OK;
 }
 
@@ -596,8 +660,11 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
     if (batch > 1 && frame_stride < (size_t)stride * h) return set_err(c, MDX_EINVAL, "frame_stride too small");
     if (P.fit_mode == MDX_FIT_EXTERNAL && !d_Hext) return set_err(c, MDX_EINVAL, "fit_mode EXTERNAL needs H_external");
     HIP_OR_RETURN(c, hipSetDevice(c->device));
+    // call pipelining: this call's pyramids go to the half the previous call did not use, and its
+    // front end runs on the front stream once that half's last reader (two calls back) is done
+    const bool pipe = may_overlap && P.call_pipelining && c->aux && c->lk_impl == 2;
     Geometry g = make_geometry(w, h, P.max_level);
-    int rc = ensure_workspace(c, g, batch);
+    int rc = ensure_workspace(c, g, batch, pipe);
     if (rc != MDX_OK) return rc;
     const int npts = mdx_grid_count(w, h, P.pixel_step);
     const int ny = (h + P.pixel_step - 1) / P.pixel_step;
@@ -608,9 +675,6 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
     uint8_t* pyr2 = c->pyr2.as<uint8_t>();
     uint32_t* der = c->der.as<uint32_t>();
     PairFit* fits = c->fits.as<PairFit>();
-    // call pipelining: this call's pyramids go to the half the previous call did not use, and its
-    // front end runs on the front stream once that half's last reader (two calls back) is done
-    const bool pipe = may_overlap && c->pipe && c->aux && c->lk_impl == 2;
     hipStream_t fs_ = s;
     int half = 0;
     if (pipe) {
@@ -621,9 +685,17 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         fs_ = c->aux;
         HIP_OR_RETURN(c, hipStreamWaitEvent(fs_, c->pyr_free[half], 0));
     }
+    if ((rc = wait_input(c, fs_)) != MDX_OK) return rc;
     c->last_pyr1 = pyr1;
     c->last_pyr2 = pyr2;
-    c->last_half = half;
+    // a row band's fit/warp reads these pyramids; any other call voids the band's
+    if (cand) {
+        c->band_pyr1 = pyr1;
+        c->band_pyr2 = pyr2;
+        c->band_half = half;
+    } else {
+        c->band_w = c->band_h = 0;
+    }
 
     mark(c, 0, fs_);
     // The class planes and A sums need only the first frames' pyramids: build those first and let
@@ -919,7 +991,8 @@ extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int n
     HIP_OR_RETURN(c, hipSetDevice(c->device));
     const int npairs = nimg - 1;
     const Geometry g = make_geometry(w, h, c->prm.max_level);
-    if ((rc = ensure_workspace(c, g, npairs)) != MDX_OK) return rc;
+    if ((rc = ensure_workspace(c, g, npairs, false)) != MDX_OK) return rc;
+    c->band_w = c->band_h = 0;   // the slabs are rebuilt: a pending band fit/warp has nothing to read
     const size_t fbytes = (size_t)stride * h;
     if ((rc = ensure(c, c->tin, fbytes * nimg)) != MDX_OK) return rc;
     hipStream_t s = c->stream;
@@ -961,17 +1034,23 @@ static int ring_grow(mdx_ctx* c, const Geometry& g, int cap)
     if (hipMalloc(&nd.p, (size_t)g.der_words * 4 * cap) != hipSuccess) return fail("hipMalloc(derivatives)");
     np.cap = (size_t)g.img_bytes * cap;
     nd.cap = (size_t)g.der_words * 4 * cap;
-    // the held frames move to slots 0 .. n-1, in order
+    // the held frames move to slots 0 .. n-1, in order; the context's state changes only once
+    // every copy has landed (a failed copy leaves the old ring intact and frees the new buffers)
+    std::vector<int> order(c->ring_order.size());
     for (size_t k = 0; k < c->ring_order.size(); k++) {
         const int o = c->ring_order[k];
-        HIP_OR_RETURN(c, hipMemcpyAsync(np.as<uint8_t>() + (size_t)g.img_bytes * k, c->ring_pyr.as<uint8_t>() + (size_t)g.img_bytes * o,
-                                        g.img_bytes, hipMemcpyDeviceToDevice, c->stream));
-        HIP_OR_RETURN(c, hipMemcpyAsync(nd.as<uint8_t>() + (size_t)g.der_words * 4 * k,
-                                        c->ring_der.as<uint8_t>() + (size_t)g.der_words * 4 * o, (size_t)g.der_words * 4,
-                                        hipMemcpyDeviceToDevice, c->stream));
-        c->ring_order[k] = (int)k;
+        if (hipMemcpyAsync(np.as<uint8_t>() + (size_t)g.img_bytes * k, c->ring_pyr.as<uint8_t>() + (size_t)g.img_bytes * o,
+                           g.img_bytes, hipMemcpyDeviceToDevice, c->stream) != hipSuccess ||
+            hipMemcpyAsync(nd.as<uint8_t>() + (size_t)g.der_words * 4 * k,
+                           c->ring_der.as<uint8_t>() + (size_t)g.der_words * 4 * o, (size_t)g.der_words * 4,
+                           hipMemcpyDeviceToDevice, c->stream) != hipSuccess) {
+            (void)hipStreamSynchronize(c->stream);
+            return fail("slot copy failed");
+        }
+        order[k] = (int)k;
     }
-    HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail("slot copy failed");
+    c->ring_order = order;
     if (c->ring_pyr.p) (void)hipFree(c->ring_pyr.p);
     if (c->ring_der.p) (void)hipFree(c->ring_der.p);
     c->ring_pyr = np;
@@ -1150,6 +1229,7 @@ extern "C" int mdx_warp_diff_dev(mdx_ctx* c, int batch, const uint8_t* d_gray1, 
     if (rc != MDX_OK) return rc;
     hipStream_t s = c->stream;
     PairFit* fits = c->fits.as<PairFit>();
+    if ((rc = wait_input(c, s)) != MDX_OK) return rc;
     for (int i = 0; i < 5; i++) mark(c, i);
     HIP_OR_RETURN(c, launch_set_fit_external(s, batch, d_H, fits));
     mark(c, 5);
@@ -1191,27 +1271,29 @@ extern "C" int mdx_band_fit_warp_dev(mdx_ctx* c, int nrec, const mdx_band_cand* 
     if (!c) return MDX_EINVAL;
     if (nrec <= 0 || !d_cands || !d_mask_band) return set_err(c, MDX_EINVAL, "mdx_band_fit_warp_dev: bad argument");
     const int w = c->band_w, h = c->band_h;
-    if (w <= 0 || h <= 0) return set_err(c, MDX_EINVAL, "mdx_band_fit_warp_dev: no mdx_band_flow_dev before");
+    if (w <= 0 || h <= 0)
+        return set_err(c, MDX_EINVAL, "mdx_band_fit_warp_dev: no mdx_band_flow_dev before, or another call rebuilt "
+                                      "the context's pyramids since");
     if (y0 < 0 || y1 > h || y0 >= y1) return set_err(c, MDX_EINVAL, "bad band [%d, %d) of %d rows", y0, y1, h);
     HIP_OR_RETURN(c, hipSetDevice(c->device));
     const Geometry g = make_geometry(w, h, c->prm.max_level);
     hipStream_t s = c->stream;
     PairFit* fits = c->fits.as<PairFit>();
-    if (!c->last_pyr1 || !c->band_img1) return set_err(c, MDX_EINVAL, "mdx_band_fit_warp_dev: no mdx_band_flow_dev before");
+    if (!c->band_pyr1 || !c->band_img1) return set_err(c, MDX_EINVAL, "mdx_band_fit_warp_dev: no mdx_band_flow_dev before");
     HIP_OR_RETURN(c, launch_band_fit(s, nrec, d_cands, fits, w, h, y0, y1));
     const Level& L0 = g.lv[0];
     // the band's flow built frame 1's pyramid for its own rows only: the rows this band's warp
     // reads beyond them (the fit is known now) are converted from the frame
     HIP_OR_RETURN(c, launch_gray_rows(s, c->band_img1, w, h, c->band_stride, c->band_fmt,
-                                      c->last_pyr1 + L0.img_off + L0.core(), L0.pitch, fits, c->band_built[0],
+                                      c->band_pyr1 + L0.img_off + L0.core(), L0.pitch, fits, c->band_built[0],
                                       c->band_built[1]));
-    const uint8_t* g1 = c->last_pyr1 + L0.img_off + L0.core();
-    const uint8_t* g2 = c->last_pyr2 + L0.img_off + L0.core();
+    const uint8_t* g1 = c->band_pyr1 + L0.img_off + L0.core();
+    const uint8_t* g2 = c->band_pyr2 + L0.img_off + L0.core();
     HIP_OR_RETURN(c, launch_warp_diff(s, 1, g1, g.img_bytes, L0.pitch, g2, g.img_bytes, L0.pitch, w, h, fits, d_mask_band,
                                       (long long)w * (y1 - y0), c->prm.thresh, y0, y1));
     if (d_H || d_num_vectors) HIP_OR_RETURN(c, launch_export_fit(s, 1, fits, d_H, d_num_vectors));
     // the band's pyramids have been read: the pipelined call two calls on may overwrite them
-    if (c->pipe) HIP_OR_RETURN(c, hipEventRecord(c->pyr_free[c->last_half], s));
+    if (c->prm.call_pipelining) HIP_OR_RETURN(c, hipEventRecord(c->pyr_free[c->band_half], s));
     else release_pyr_all(c);
     return MDX_OK;
 }

@@ -108,6 +108,11 @@ struct LkArgs {
                              // the level launches run one after another
     int done_stride;
     int dep_groups;          // > 0: groups per pair of the coarser level, which a group waits for
+    int* err;                // dataflow: [0] group waits, [1] gate waits that timed out (read and
+                             // cleared at the context's sync points: mdx_sync returns MDX_EHIP)
+    int spin_max;            // dataflow wait bound in s_sleep(8) polls; < 0: fault injection (every
+                             // wait counts as timed out at once; tests)
+    int flow_cap;            // dataflow: percent of the resident waves one iteration launch takes
     float4* dbg;             // optional [batch][nlev][npts] (npx, npy, iters, status) at level end
     int dbg_pt;              // point whose per-iteration values are appended after dbg (pair 0)
 };
@@ -117,6 +122,8 @@ struct LkArgs {
 // running launches update and poll, and the dataflow ran 1.4-3x slower wherever the batch did not
 // fill whole lines (8, 16, 24, 40 pairs) -- the concurrent launches contending on shared lines.
 constexpr int kCtrPad = 32;
+// default dataflow wait bound: s_sleep(8) polls, ~0.1 s
+constexpr int kLkSpinDefault = 1 << 19;
 
 // Core rows [lo, hi) of one pyramid level (row-band mode: what a band's LK reads)
 struct RowSpan {

@@ -137,10 +137,10 @@ __device__ __forceinline__ void wave_lds_fence()
 #ifndef MDX_LK_NB
 #define MDX_LK_NB 2
 #endif
-// dataflow waits: at most this many s_sleep(8) polls (~0.1 s) before a group proceeds regardless
-// (and its wave stops waiting altogether): a wait that long means the hand-off failed, and the
-// results are then wrong rather than the launch hung
-constexpr int kLkSpinMax = 1 << 19;
+// Dataflow waits are bounded (LkArgs::spin_max s_sleep(8) polls, ~0.1 s by default): past that a
+// group proceeds regardless and its wave stops waiting, so the launch drains instead of hanging.
+// Every such give-up is counted in LkArgs::err, which the host reads at its next sync point and
+// turns into MDX_EHIP: a timed-out hand-off is never a silent wrong result.
 #ifndef MDX_LK_RFIRST
 #define MDX_LK_RFIRST 0
 #endif
@@ -665,8 +665,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                                 // waiting waves polling one line would load its L2 channel
                                 const int* d = a.done + ((level + 1) * a.done_stride + pair) * kCtrPad;
                                 int slept = 0, gap = 1;
-                                while (__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.dep_groups) {
-                                    if (slept >= kLkSpinMax) {
+                                if (a.spin_max < 0) gave_up = true;   // fault injection (tests)
+                                while (!gave_up &&
+                                       __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.dep_groups) {
+                                    if (slept >= a.spin_max) {
                                         gave_up = true;
                                         break;
                                     }
@@ -674,7 +676,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                                     slept += gap;
                                     gap = gap < 16 ? 2 * gap : 16;
                                 }
+                                if (gave_up)   // this slot's results may be wrong: say so
+                                    __hip_atomic_fetch_add(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             }
+                            // The hand-off is MI355X_MICROARCH.md's measured form (table row 1):
+                            // every carried point stored sc1, each storing wave's vmcnt(0) before
+                            // one lane's agent atomic add, the consumer's sc1 poll, then sc1
+                            // loads only -- no acquire fence needed.  This compiler-only fence
+                            // (wavefront scope: no instruction) keeps the loads below the poll.
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                             if (q.valid)
                                 p = __builtin_bit_cast(float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(a.next_pts) + po,
                                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -898,22 +908,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
 // dispatched only into the slots the tail frees, and find ready work there.  Without the gate the
 // next level, launched beside the coarser level's whole queue, took half the chip and spun (both
 // launches ~2x slower); gated on the queues alone, one pair per XCD (4K x 8) left every next-level
-// wave polling its pair's counter (LK 3x slower).  Bounded like the group waits.
+// wave polling its pair's counter (LK 3x slower).  Bounded like the group waits, and counted the
+// same way when the bound is hit (err[1]).
 __global__ __launch_bounds__(64) void k_lk_gate(const int* __restrict__ qctr, long long T, const int* __restrict__ done,
-                                                int dep_groups, int ngroups_next, long long T_next)
+                                                int dep_groups, int ngroups_next, long long T_next, int* __restrict__ err,
+                                                int spin_max)
 {
     const int x = threadIdx.x;
     if (x >= 8) return;
     const long long cb = T * x / 8, ce = T * (x + 1) / 8;
     const long long cbn = T_next * x / 8;
     const int pf = cbn < T_next ? (int)(cbn / ngroups_next) : -1;
-    for (int t = 0; t < kLkSpinMax; t++) {
+    bool ready = false;
+    for (int t = 0; t < spin_max; t++) {
         const bool dry = __hip_atomic_load(qctr + x * kCtrPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ce - cb;
         const bool first =
             pf < 0 || __hip_atomic_load(done + pf * kCtrPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= dep_groups;
-        if (dry && first) break;
+        if (dry && first) {
+            ready = true;
+            break;
+        }
         __builtin_amdgcn_s_sleep(8);
     }
+    if (!ready) __hip_atomic_fetch_add(err + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // persistent waves for k_lk_iter: what the current device keeps resident at once (cached per
@@ -934,17 +951,6 @@ static int lk_iter_resident()
         if (dev >= 0 && dev < kDevs) cached[dev].store(v, std::memory_order_relaxed);
     }
     return v;
-}
-
-// dataflow launches: percent of the resident waves each iteration launch takes (MDX_LK_CAP)
-static int lk_flow_cap()
-{
-    static const int cap = [] {
-        const char* e = std::getenv("MDX_LK_CAP");
-        const int v = e ? std::atoi(e) : 85;
-        return v < 10 ? 10 : v > 100 ? 100 : v;
-    }();
-    return cap;
 }
 
 template <int G, int UW>
@@ -974,7 +980,7 @@ static void launch_iter(hipStream_t s, int batch, const LkArgs& a, const uint8_t
     // launch that this one may wait on
     const int need = (int)std::min<long long>(((long long)batch * ngroups + S - 1) / S, 1 << 30);
     int res = lk_iter_resident<G, UW>();
-    if (a.done) res = res * lk_flow_cap() / 100;
+    if (a.done) res = res * std::min(std::max(a.flow_cap, 10), 100) / 100;   // the context's (MDX_LK_CAP)
     const int W = std::max(8, std::min((need + 7) / 8, res / 8) * 8);
     hipLaunchKernelGGL((k_lk_iter<G, UW>), dim3(W), dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups, batch);
 }
@@ -1053,7 +1059,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         // no two pairs' carried points may share a 128-B line; with one pair per XCD (batch 8) the
         // next level can only start once the whole level is done there, and the dataflow measured
         // 1.5% slower than levels in sequence, so it needs at least two
-        const bool flow = aux && s2 && flow_ev && done && nb % 8 == 0 && nb >= 16 && a.npts % 16 == 0 &&
+        const bool flow = aux && s2 && flow_ev && done && a.err && nb % 8 == 0 && nb >= 16 && a.npts % 16 == 0 &&
                           (reinterpret_cast<uintptr_t>(b.next_pts) & 127) == 0;
         if (flow) {
             if (hipError_t e = hipMemsetAsync(done, 0, sizeof(int) * kMaxLevels * nb * kCtrPad, s)) return e;
@@ -1080,7 +1086,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
                 const int ng = (C.nxp / C.G) * a.nyg;
                 hipLaunchKernelGGL(k_lk_gate, dim3(1), dim3(64), 0, st, bq + (l + 1) * 8 * kCtrPad,
                                    (long long)nb * bl.dep_groups, done + (l + 1) * nb * kCtrPad, bl.dep_groups, ng,
-                                   (long long)nb * ng);
+                                   (long long)nb * ng, a.err, a.spin_max);
             }
             const float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             switch (C.G * 1000 + C.UW) {

@@ -224,11 +224,10 @@ def test_row_tiled_matches_full(mdx, monkeypatch, w, h, ps, nb, ch, pipe):
     """Row bands run one after another on one GPU, records exchanged through
     host memory: every point, the fit, the count and every mask row equal the full path's (also
     with call pipelining, whose band calls alternate pyramid halves)."""
-    monkeypatch.setenv("MDX_PIPE", pipe)
     from motion_detection_amd import rowtile
     a, b, _ = mdx.synth_pair(7000 + nb, w, h, ch)
     fmt = mdx.FMT_GRAY8 if ch == 1 else mdx.FMT_RGB8
-    with mdx.Context(0, w, h, 1, pixel_step=ps, min_vector_size=1.0) as c:
+    with mdx.Context(0, w, h, 1, pixel_step=ps, min_vector_size=1.0, call_pipelining=int(pipe)) as c:
         full = c.flow_warp_diff(a, b, fmt=fmt)
         n = mdx.grid_count(w, h, ps)
         stride = w * ch
@@ -308,19 +307,18 @@ def test_full_path_8k_rgb_bit_exact(mdx, oracle):
     _compare(res, ref, "8k rgb")
 
 
-@pytest.mark.parametrize("env", [{"MDX_PIPE": "1"}, {}])
-def test_back_to_back_calls_pipelined(mdx, oracle, monkeypatch, env):
+@pytest.mark.parametrize("pipe", [1, 0])
+def test_back_to_back_calls_pipelined(mdx, oracle, pipe):
     """Calls enqueued back to back without a host sync (the bench's pattern): with call pipelining
-    (MDX_PIPE=1, inputs resident before each call) each call's front end runs beside the previous
-    call's last level and fit/warp, on the other half of the pyramid slabs.  Four calls on three different batches into separate outputs, a
-    synchronous trajectory call in between: every call's results equal the oracle's."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    (mdx_params.call_pipelining, inputs resident before each call) each call's front end runs beside
+    the previous call's last level and fit/warp, on the other half of the pyramid slabs.  Four calls
+    on three different batches into separate outputs, a synchronous trajectory call in between:
+    every call's results equal the oracle's."""
     w, h, B = 320, 240, 8
     n = mdx.grid_count(w, h, 10)
     sets = [[mdx.synth_pair(700 + 10 * s + i, w, h, 1) for i in range(B)] for s in range(3)]
     order = [0, 1, 2, 0]
-    with mdx.Context(0, w, h, B) as c:
+    with mdx.Context(0, w, h, B, call_pipelining=pipe) as c:
         c.set_params(pixel_step=10)
         ins = []
         for pairs in sets:
@@ -368,12 +366,11 @@ def test_row_bands_on_separate_contexts(mdx, monkeypatch, w, h, ps, nb, ch, pipe
     """Each band on its own context, as on its own GPU: a band's flow builds frame 1's pyramid for
     its rows only, so the rows its warp reads beyond the band (camera motion) come from the frame
     at fit/warp time.  Every mask row equals the full path's (also with call pipelining)."""
-    monkeypatch.setenv("MDX_PIPE", pipe)
     from motion_detection_amd import rowtile
     a, b, _ = mdx.synth_pair(7100 + nb, w, h, ch)
     fmt = mdx.FMT_GRAY8 if ch == 1 else mdx.FMT_RGB8
     n = mdx.grid_count(w, h, ps)
-    ctxs = [mdx.Context(0, w, h, 1, pixel_step=ps, min_vector_size=1.0) for _ in range(nb)]
+    ctxs = [mdx.Context(0, w, h, 1, pixel_step=ps, min_vector_size=1.0, call_pipelining=int(pipe)) for _ in range(nb)]
     try:
         full = ctxs[0].flow_warp_diff(a, b, fmt=fmt)
         recs = np.empty(nb, rowtile.BAND_CAND_DTYPE)
