@@ -137,23 +137,29 @@ def stamped_pmc(path: str, key: str, expect: str):
     return pj
 
 
-def cpu_baseline(uniq, w, h, seconds: float, threads: int):
+def cpu_baseline(uniq, w, h, seconds: float, threads: int, simd: bool = True):
     """The C oracle on this host: whole reference path per pair, `threads` threads over LK
-    points / warp rows (like OpenCV's parallel_for_).  Bounded sample: pairs are processed
-    until `seconds` of wall time have elapsed (at least one)."""
+    points / warp rows (like OpenCV's parallel_for_).  simd: the LK sums and the warp's bilinear
+    through the SSE2 restatement (oracle/mdx_oracle_sse2.c, OpenCV 2.4's own x86 lane order, same
+    results), which is what the reference's x86 OpenCV build runs; otherwise the scalar loops.
+    Bounded sample: pairs are processed until `seconds` of wall time have elapsed (at least one)."""
     from oracle import pyoracle
     pyoracle.build()
     n, t0 = 0, time.perf_counter()
     while True:
         a, b, _ = uniq[n % len(uniq)]
-        pyoracle.calculate_optical_flow(a, b, nthreads=threads, pixel_step=10, min_vector_size=1.0)
+        pyoracle.calculate_optical_flow(a, b, nthreads=threads, pixel_step=10, min_vector_size=1.0, simd=simd)
         n += 1
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return dict(value=round(n * w * h / 1e6 / el, 3), unit="Mpixels/s", cores=threads, kind="port",
-                sample=f"{n} x {w}x{h} gray pairs, full reference path (oracle/mdx_oracle.c, scalar C restatement of "
-                       f"the OpenCV 2.4 path, {threads} thread(s) over LK points / warp rows), {el:.1f} s wall")
+    what = ("SSE2-intrinsics restatement of the OpenCV 2.4 x86 path (oracle/mdx_oracle_sse2.c: LK window/iteration "
+            "sums and warp bilinear in 4-lane vectors; pyramids, Scharr and fit scalar, <3% of the time)"
+            if simd else "scalar C restatement of the OpenCV 2.4 path (oracle/mdx_oracle.c)")
+    return dict(value=round(n * w * h / 1e6 / el, 3), unit="Mpixels/s", cores=threads,
+                kind="port-sse2" if simd else "port",
+                sample=f"{n} x {w}x{h} gray pairs, full reference path ({what}, {threads} thread(s) over LK points / "
+                       f"warp rows), {el:.1f} s wall")
 
 
 def check_outputs(uniq, outs, B, w, h, ps, threads):
@@ -163,7 +169,7 @@ def check_outputs(uniq, outs, B, w, h, ps, threads):
     num_vectors.  Returns the counts; a mismatch is reported in the line, never hidden."""
     from oracle import pyoracle
     pyoracle.build()
-    refs = [pyoracle.calculate_optical_flow(a, b, nthreads=threads, pixel_step=ps, min_vector_size=1.0)
+    refs = [pyoracle.calculate_optical_flow(a, b, nthreads=threads, pixel_step=ps, min_vector_size=1.0, simd=True)
             for a, b, _ in uniq]
     bad = []
     for i in range(B):
@@ -515,7 +521,7 @@ def main():
     ap.add_argument("--roofline-batch", type=int, default=32)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--only-roofline", action="store_true", help="profiling aid: only the warp+diff roofline leg")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="per CPU-baseline leg (nproc threads, 1 thread)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="main CPU-baseline leg (all CPUs, SSE2); the 1-core and scalar legs take half")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_warp_diff.json"),
                     help="per-launch HBM traffic measured by rocprofv3 --pmc (scripts/profile.sh)")
@@ -686,12 +692,13 @@ def main():
     parity = None
     if not args.only_roofline and not args.no_parity:
         parity = check_outputs(uniq, outs, B, w, h, ps, host_cores()["available"])
-    cpu = cpu1 = None
+    cpu = cpu1 = cpu_scalar = None
     if D.world == 1 and not args.no_cpu:
         hc = host_cores()
-        cpu = cpu_baseline(uniq, w, h, args.cpu_seconds, hc["available"])   # every CPU this job may use
+        cpu = cpu_baseline(uniq, w, h, args.cpu_seconds, hc["available"])   # every CPU this job may use, SSE2
         cpu.update(nproc=hc["nproc"], cgroup_cpu_quota=hc["cgroup_cpu_quota"])
-        cpu1 = cpu_baseline(uniq, w, h, args.cpu_seconds, 1)             # one core
+        cpu1 = cpu_baseline(uniq, w, h, args.cpu_seconds / 2, 1)          # one core, SSE2
+        cpu_scalar = cpu_baseline(uniq, w, h, args.cpu_seconds / 2, hc["available"], simd=False)
     live = None
     if D.world == 1 and not args.no_live and not args.only_roofline:
         live = live_leg(D.local_rank, w, h, threads, with_cpu=not args.no_cpu)
@@ -737,6 +744,7 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "cpu_baseline_1core": cpu1,
+        "cpu_baseline_scalar": cpu_scalar,
         "ranks": devs["ranks"],
         "devices": devs["devices"],
         "build": mdx._lib.build_info(),

@@ -190,6 +190,9 @@ void ora_free_pyramid(ora_pyramid* p)
 /* ---------------------------------------------------------------- A5: LK tracker ------ */
 /* cvRound(float) == _mm_cvtss_si32 (round half to even); cvFloor via double. */
 static inline int cv_round_f(float v) { return (int)lrintf(v); }
+
+static int g_simd = 0;
+void ora_set_simd(int on) { g_simd = on != 0; }
 static inline int cv_floor_f(float v) { return (int)floor((double)v); }
 
 typedef struct {
@@ -258,6 +261,10 @@ static void lk_level_range(const lk_job* jb)
         int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
 
         float qA11[4] = {0, 0, 0, 0}, qA12[4] = {0, 0, 0, 0}, qA22[4] = {0, 0, 0, 0};
+        if (g_simd && win % 4 == 0)
+            ora_sse2_window_sums(I0 + (ptrdiff_t)ipy * stepI + ipx, stepI, D0 + (ptrdiff_t)ipy * dstep + (ptrdiff_t)ipx * 2,
+                                 dstep, win, iw00, iw01, iw10, iw11, Iwin, dIwin, qA11, qA12, qA22);
+        else
         for (int y = 0; y < win; y++) {
             const uint8_t* src = I0 + (ptrdiff_t)(y + ipy) * stepI + ipx;
             const int16_t* dsrc = D0 + (ptrdiff_t)(y + ipy) * dstep + (ptrdiff_t)ipx * 2;
@@ -309,6 +316,9 @@ static void lk_level_range(const lk_job* jb)
             iw10 = cv_round_f((1.f - a) * b * (float)(1 << W_BITS));
             iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
             float q1[4] = {0, 0, 0, 0}, q2[4] = {0, 0, 0, 0};
+            if (g_simd && win % 4 == 0)
+                ora_sse2_iter_sums(J0 + (ptrdiff_t)iny * stepJ + inx, stepJ, Iwin, dIwin, win, iw00, iw01, iw10, iw11, q1, q2);
+            else
             for (int y = 0; y < win; y++) {
                 const uint8_t* Jp = J0 + (ptrdiff_t)(y + iny) * stepJ + inx;
                 const int16_t* Ip = Iwin + y * win;
@@ -702,6 +712,29 @@ static void warp_rows(const warp_job* jb)
             double Y0 = M[3] * xb + M[4] * y + M[5];
             double W0 = M[6] * xb + M[7] * y + M[8];
             for (int x1 = 0; x1 < bw; x1++) {
+                if (g_simd && x1 + 4 <= bw) {
+                    /* four pixels at once when all their taps are inside (remapBilinear's vector
+                     * loop over interior runs); otherwise this pixel takes the scalar code below */
+                    const uint8_t* pp[4];
+                    int wt4[4][4], k;
+                    for (k = 0; k < 4; k++) {
+                        double Wk = W0 + M[6] * (x1 + k);
+                        Wk = Wk != 0 ? 32.0 / Wk : 0;
+                        double fX = (X0 + M[0] * (x1 + k)) * Wk, fY = (Y0 + M[3] * (x1 + k)) * Wk;
+                        fX = fX < (double)INT_MIN ? (double)INT_MIN : fX > (double)INT_MAX ? (double)INT_MAX : fX;
+                        fY = fY < (double)INT_MIN ? (double)INT_MIN : fY > (double)INT_MAX ? (double)INT_MAX : fY;
+                        int X = (int)lrint(fX), Y = (int)lrint(fY);
+                        int sx = sat_short(X >> 5), sy = sat_short(Y >> 5);
+                        if (!((unsigned)sx < (unsigned)(W - 1) && (unsigned)sy < (unsigned)(H - 1))) break;
+                        pp[k] = jb->src + (size_t)sy * jb->sstride + sx;
+                        bilinear_tab(X & 31, Y & 31, wt4[k]);
+                    }
+                    if (k == 4) {
+                        ora_sse2_bilinear4(pp, jb->sstride, (const int(*)[4])wt4, d + xb + x1);
+                        x1 += 3;
+                        continue;
+                    }
+                }
                 double Wd = W0 + M[6] * x1;
                 Wd = Wd != 0 ? 32.0 / Wd : 0;
                 double fX = (X0 + M[0] * x1) * Wd;

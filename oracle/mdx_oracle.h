@@ -71,6 +71,17 @@ void ora_lk(const ora_pyramid* prev, const ora_pyramid* next, int max_level,
 
 /* 1: JacobiSVDImpl_ with SSE2 VBLAS dot/givensx partial sums (see mdx_oracle.c); 0: scalar (default) */
 void ora_set_svd_vblas(int on);
+/* 1: the LK window / iteration sums and the warp's interior bilinear run the SSE2-intrinsics
+ * restatement (mdx_oracle_sse2.c, OpenCV 2.4's x86 4-lane order, bit-identical results); 0: the
+ * scalar loops.  The timed CPU baseline uses 1. */
+void ora_set_simd(int on);
+/* mdx_oracle_sse2.c (internal) */
+void ora_sse2_window_sums(const uint8_t* I, int stepI, const int16_t* D, int dstep, int win, int iw00, int iw01,
+                          int iw10, int iw11, int16_t* Iwin, int16_t* dIwin, float qA11[4], float qA12[4],
+                          float qA22[4]);
+void ora_sse2_iter_sums(const uint8_t* J, int stepJ, const int16_t* Iwin, const int16_t* dIwin, int win, int iw00,
+                        int iw01, int iw10, int iw11, float q1[4], float q2[4]);
+void ora_sse2_bilinear4(const uint8_t* const p[4], int stride, const int w[4][4], uint8_t out[4]);
 void ora_get_perspective_transform(const float src[8], const float dst[8], double M[9]);
 int  ora_invert3x3(const double M[9], double Minv[9]);
 void ora_warp_perspective(const uint8_t* src, int w, int h, int sstride, const double M[9],

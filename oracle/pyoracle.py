@@ -38,8 +38,8 @@ class OraRandState(C.Structure):
 
 def build(force: bool = False) -> str:
     """Compile the oracle with its Makefile (gcc is present on the GPU box too)."""
-    src = os.path.join(_HERE, "mdx_oracle.c")
-    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("mdx_oracle.c", "mdx_oracle_sse2.c", "mdx_oracle.h", "Makefile")]
+    if force or not os.path.exists(_LIB_PATH) or any(os.path.getmtime(_LIB_PATH) < os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
 
@@ -63,6 +63,8 @@ def lib():
         L.ora_get_perspective_transform.argtypes = [f32p, f32p, f64p]
         L.ora_set_svd_vblas.argtypes = [C.c_int]
         L.ora_set_svd_vblas.restype = None
+        L.ora_set_simd.argtypes = [C.c_int]
+        L.ora_set_simd.restype = None
         L.ora_invert3x3.argtypes = [f64p, f64p]
         L.ora_invert3x3.restype = C.c_int
         L.ora_warp_perspective.argtypes = [u8p, C.c_int, C.c_int, C.c_int, f64p, u8p, C.c_int, C.c_int]
@@ -178,9 +180,16 @@ def grid_count(w: int, h: int, ps: int) -> int:
     return lib().ora_grid_count(w, h, ps)
 
 
+def set_simd(on: bool) -> None:
+    """Select the oracle's hot loops: False (default) scalar C, True the SSE2-intrinsics restatement
+    (oracle/mdx_oracle_sse2.c; OpenCV 2.4's x86 lane order, bit-identical results)."""
+    lib().ora_set_simd(1 if on else 0)
+
+
 def calculate_optical_flow(img1: np.ndarray, img2: np.ndarray, fmt: int | None = None, nthreads: int = 1,
-                           want_mask: bool = True, **kw):
-    """Whole reference path.  Returns dict like motion_detection_amd's result."""
+                           want_mask: bool = True, simd: bool = False, **kw):
+    """Whole reference path.  Returns dict like motion_detection_amd's result.  simd: run the LK
+    sums and the warp's bilinear through the SSE2 restatement (same results, CPU-baseline speed)."""
     img1 = np.ascontiguousarray(img1)
     img2 = np.ascontiguousarray(img2)
     h, w = img1.shape[:2]
@@ -195,10 +204,14 @@ def calculate_optical_flow(img1: np.ndarray, img2: np.ndarray, fmt: int | None =
     H = np.zeros(9)
     Hinv = np.zeros(9)
     fs = C.c_int(0)
-    num = lib().ora_calculate_optical_flow(
-        _p(img1, C.c_uint8), _p(img2, C.c_uint8), w, h, img1.strides[0], fmt, C.byref(prm), nthreads,
-        _p(nextp, C.c_float), _p(status, C.c_uint8), _p(vec, C.c_double),
-        _p(mask, C.c_uint8) if mask is not None else None, _p(H, C.c_double), _p(Hinv, C.c_double), C.byref(fs))
+    lib().ora_set_simd(1 if simd else 0)
+    try:
+        num = lib().ora_calculate_optical_flow(
+            _p(img1, C.c_uint8), _p(img2, C.c_uint8), w, h, img1.strides[0], fmt, C.byref(prm), nthreads,
+            _p(nextp, C.c_float), _p(status, C.c_uint8), _p(vec, C.c_double),
+            _p(mask, C.c_uint8) if mask is not None else None, _p(H, C.c_double), _p(Hinv, C.c_double), C.byref(fs))
+    finally:
+        lib().ora_set_simd(0)
     return dict(num_vectors=num, next_pts=nextp, status=status, vectors=vec, mask=mask,
                 H=H.reshape(3, 3), Hinv=Hinv.reshape(3, 3), fit_status=fs.value)
 

@@ -31,14 +31,17 @@ def _golden_names():
         return sorted(json.load(f))
 
 
+@pytest.mark.parametrize("simd", [False, True], ids=["scalar", "sse2"])
 @pytest.mark.parametrize("name", _golden_names())
-def test_oracle_matches_golden(oracle, name):
+def test_oracle_matches_golden(oracle, name, simd):
+    """Both oracle modes (the scalar C loops and the SSE2 restatement timed as the CPU baseline)
+    reproduce every committed golden vector."""
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         man = json.load(f)[name]
     g = np.load(os.path.join(GOLDEN, name + ".npz"))
     assert _sha(g["img1"], g["img2"]) == man["inputs_sha256"]
     r = oracle.calculate_optical_flow(g["img1"], g["img2"], pixel_step=int(g["pixel_step"]),
-                                      min_vector_size=float(g["min_vector_size"]))
+                                      min_vector_size=float(g["min_vector_size"]), simd=simd)
     assert r["num_vectors"] == int(g["num_vectors"]) == man["num_vectors"]
     assert np.array_equal(r["status"], g["status"])
     assert np.array_equal(r["next_pts"].view(np.uint32), g["next_pts"].view(np.uint32))
@@ -78,6 +81,21 @@ def test_oracle_matches_numpy_restatement(oracle, seed, w, h, ps, ch):
     assert np.array_equal(r["vectors"], c["vectors"])
     assert np.array_equal(r["H"], c["H"])
     assert np.array_equal(r["mask"], c["mask"])
+
+
+@pytest.mark.parametrize("w,h,ps,ch,seed", [(1920, 1080, 10, 1, 20141105), (1920, 1080, 10, 1, 20141108),
+                                             (640, 480, 3, 3, 7), (333, 241, 7, 1, 11), (81, 83, 1, 1, 31)])
+def test_sse2_oracle_equals_scalar(oracle, w, h, ps, ch, seed):
+    """The SSE2 restatement (oracle/mdx_oracle_sse2.c; OpenCV 2.4's x86 lane order) against the
+    scalar loops, bit for bit, on the bench's 1080p pairs and other geometries: the CPU baseline
+    times the same arithmetic the GPU is checked against."""
+    import motion_detection_amd as m
+    a, b, _ = m.synth_pair(seed, w, h, ch, 8)
+    r = oracle.calculate_optical_flow(a, b, nthreads=8, pixel_step=ps, min_vector_size=1.0)
+    s = oracle.calculate_optical_flow(a, b, nthreads=8, pixel_step=ps, min_vector_size=1.0, simd=True)
+    assert r["num_vectors"] == s["num_vectors"]
+    for k in ("next_pts", "status", "vectors", "H", "mask"):
+        assert np.array_equal(np.asarray(r[k]).view(np.uint8), np.asarray(s[k]).view(np.uint8)), k
 
 
 # ---------------------------------------------------------------- known-answer tests
