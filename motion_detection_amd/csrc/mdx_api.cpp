@@ -74,6 +74,7 @@ struct mdx_ctx {
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
     int lk_sub = 0;                          // > 0: LK sub-batch cap (MDX_LK_SUB, tests)
+    bool lk_arows = true;                    // A sums per row strip where the plan allows (MDX_LK_AROWS=0: per group)
     int plan_w = -1, plan_h = -1, plan_ps = -1, plan_ml = -1, plan_gy0 = -1, plan_gy1 = -1;
     int band_w = 0, band_h = 0;              // frame of the last mdx_band_flow_dev (its pyramids are live)
     ClassPlan plan{};
@@ -287,6 +288,33 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
             const int16_t* cmy = cmap + (l * 2 + 1) * 128;
             std::stable_sort(ord.begin() + r0, ord.end(),
                              [&](int16_t u, int16_t v) { return cmy[(u * ps) & m] < cmy[(v * ps) & m]; });
+            // A-sum strips (k_lk_A_rows): runs of one y-class cut into kAStripRows rows; the first
+            // window rows v0 = ipy + 40 of a class's rows must be evenly spaced (asp rows apart)
+            const size_t r1 = ord.size();
+            auto v0_row = [&](int gy) { return (int)std::floor((float)(gy * ps) * scale - 19.5f) + kPad; };
+            int asp = 0;
+            bool uniform = true;
+            std::vector<int16_t> strips;
+            for (size_t i = r0; i < r1;) {
+                size_t e = i + 1;
+                const int cls = cmy[(ord[i] * ps) & m];
+                while (e < r1 && cmy[(ord[e] * ps) & m] == cls) {
+                    const int d = v0_row(ord[e]) - v0_row(ord[e - 1]);
+                    if (asp == 0) asp = d;
+                    if (d != asp) uniform = false;
+                    e++;
+                }
+                for (size_t s = i; s < e; s += kAStripRows) {
+                    strips.push_back((int16_t)(s - r0));
+                    strips.push_back((int16_t)std::min<size_t>(kAStripRows, e - s));
+                }
+                i = e;
+            }
+            if (asp == 0) asp = kWin;   // one row per class: windows never overlap
+            C.asp = uniform && asp >= 5 && c->lk_arows ? asp : 0;
+            C.nstrip = (int)strips.size() / 2;
+            C.strip_off = (int)ord.size();
+            ord.insert(ord.end(), strips.begin(), strips.end());
         }
         (void)ny;
         long long off = 0;
@@ -354,6 +382,7 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     if (const char* e = std::getenv("MDX_LK_IMPL")) c->lk_impl = std::atoi(e) == 1 ? 1 : 2;
     if (const char* e = std::getenv("MDX_LK_G")) c->lk_g = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_SUB")) c->lk_sub = std::atoi(e);
+    if (const char* e = std::getenv("MDX_LK_AROWS")) c->lk_arows = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_TRAJ_CHAIN")) c->traj_chain = std::atoi(e) != 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {

@@ -61,7 +61,14 @@ struct ClassLevel {
     int G;                   // points per LK group (4 or 8)
     int UW;                  // union columns per group (64, 128, 256 or 512)
     int vlo, vhi;            // plane rows the planned grid rows' windows reach (k_lk_class range)
+    // A sums per row strip (k_lk_A_rows): the level's grid rows, in class order, cut into strips of
+    // at most kAStripRows rows of one y-class whose windows start every `asp` plane rows; 0: the
+    // per-group k_lk_A instead (spacing not uniform, or below 5 rows: too many windows overlap)
+    int asp;
+    int nstrip;              // strips (table at LkArgs::ord + strip_off: (first row index, rows) pairs)
+    int strip_off;
 };
+constexpr int kAStripRows = 16;
 
 // (G, UW) shapes of the LK level kernels (mdx_lk.hip instantiates these; the host plan picks the
 // smallest UW >= a level's union span among the shapes of its G)

@@ -521,6 +521,177 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
     if (q.valid && k == 0) Ab[(long long)pair * a.npts + q.gx * a.ny + q.gy] = make_float4(A11, A12, A22, Dinv);
 }
 
+// the gradient sums of one window (lane k: SSE lane k's partials) -> (A11, A12, A22, 1/D or 0),
+// the quad combine ((P0+P1)+P2)+P3 and LKTrackerInvoker's minEig / determinant tests
+__device__ __forceinline__ float4 lk_A_result(f2 sd, float s12, bool ok, float min_eig)
+{
+    constexpr float FLT_SCALE = 1.f / (1 << 20);
+    const float a11 = ((quad_bcast<0>(sd.x) + quad_bcast<1>(sd.x)) + quad_bcast<2>(sd.x)) + quad_bcast<3>(sd.x);
+    const float a12 = ((quad_bcast<0>(s12) + quad_bcast<1>(s12)) + quad_bcast<2>(s12)) + quad_bcast<3>(s12);
+    const float a22 = ((quad_bcast<0>(sd.y) + quad_bcast<1>(sd.y)) + quad_bcast<2>(sd.y)) + quad_bcast<3>(sd.y);
+    const float A11 = a11 * FLT_SCALE, A12 = a12 * FLT_SCALE, A22 = a22 * FLT_SCALE;
+    float Dinv = 0.f;
+    if (ok) {
+        const float D = A11 * A22 - A12 * A12;
+        const float minEig = (A22 + A11 - __builtin_sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
+                             (float)(2 * kWin * kWin);
+        if (!(minEig < min_eig || D < FLT_EPSILON)) Dinv = 1.f / D;
+    }
+    return make_float4(A11, A12, A22, Dinv);
+}
+
+// ---- A pass per row strip.  Neighbouring grid rows of one residue class have windows that start
+// `asp` plane rows apart (5 at pixel_step 10 above level 0, 10 at level 0), so every plane row lies
+// in 40 / asp of them: k_lk_A re-reads each plane row that many times.  Here a wave owns S column
+// groups (the G class members of a group, as in k_lk_A) over a strip of up to kAStripRows grid rows
+// of one y-class, streams the strip's plane rows ONCE (same LDS-DMA row images), converts each
+// element once, and adds it into the chains of every window containing the row: window j of the
+// strip lives in accumulator slot j % NW (NW * asp >= 40, so a slot's windows never overlap) from
+// its first row to its 40th, then is finished like k_lk_A's.  Each window's chains see exactly
+// k_lk_A's operands in k_lk_A's order, so the sums are the same bits.
+// grid: x -> (strip, column-group wave), y -> pair (XCD-remapped as one range)
+template <int G, int UW, int NW>
+__global__ __launch_bounds__(64) void k_lk_A_rows(LkArgs a, const uint8_t* __restrict__ cls, float4* __restrict__ Ab,
+                                                  int* __restrict__ qctr, int level, int ncg)
+{
+    using Sh = LkShape<G, UW>;
+    constexpr int LPS = Sh::LPS, S = Sh::S, ND = Sh::ND;
+    __shared__ __attribute__((aligned(16))) uint32_t img0[ND * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t img1[ND * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t img2[ND * 256];
+
+    const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
+    const int nw = gridDim.x;
+    const int bid = xcd_remap(blockIdx.x + nw * blockIdx.y, nw * gridDim.y);
+    const int pair = bid / nw, w = bid % nw;
+    if (bid == 0 && lane < 8) qctr[(level * 8 + lane) * kCtrPad] = 0;   // k_lk_iter's queue heads
+    const ClassLevel& C = a.plan.lv[level];
+    const Level L = a.g.lv[level];
+    const int ncw = (ncg + S - 1) / S;
+    const int strip = w / ncw, cg = (w - strip * ncw) * S + slot;
+    const int16_t* xo = a.ord + C.ord_off;
+    const int16_t* yo = xo + C.nxp;
+    const int r0 = a.ord[C.strip_off + 2 * strip], nr = a.ord[C.strip_off + 2 * strip + 1];
+    const int asp = C.asp;
+    const float scale = (float)(1. / (1 << level));
+    const int m = (1 << level) - 1;
+    // column geometry of this lane quad's point (group_geom's, with the strip's first row)
+    const int gx0 = cg < ncg ? xo[cg * G] : -1;
+    const int gxv = cg < ncg ? xo[cg * G + (sl >> 2)] : -1;
+    const bool valid = gxv >= 0;
+    const int gx = valid ? gxv : 0;
+    const int ipx = (int)floorf((float)(gx * a.pixel_step) * scale - 19.5f);
+    const int gy0 = yo[r0];
+    const int ipx0 = (int)floorf((float)((gx0 >= 0 ? gx0 : 0) * a.pixel_step) * scale - 19.5f);
+    const int cx = class_of(a.cmap, level, 0, ((gx0 >= 0 ? gx0 : 0) * a.pixel_step) & m);
+    const int cy = class_of(a.cmap, level, 1, (gy0 * a.pixel_step) & m);
+    const int ub = min(max(ipx0 + kPad, 0), C.PW - UW);
+    const int off = min(max(ipx + kPad - ub, 0), UW - kWin);
+    const uint32_t ubase = (uint32_t)(C.off + (long long)(cy * C.nrx + cx) * C.class_bytes) + 8u * (uint32_t)ub;
+    const int ipy0 = (int)floorf((float)(gy0 * a.pixel_step) * scale - 19.5f);
+    const int v00 = min(max(ipy0 + kPad, 0), C.UH - kWin);
+    const int R = (nr - 1) * asp + kWin;                           // plane rows of the strip
+
+    const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cls + (long long)pair * a.plan.bytes_per_pair, a.plan.bytes_per_pair);
+    const uint32_t rowb = (uint32_t)C.PW * 8;
+    uint32_t uoff[ND];
+    {
+        const uint32_t mine = ubase + (uint32_t)v00 * rowb;
+#pragma unroll
+        for (int c = 0; c < ND; c++) {
+            const int P = 1024 * c + 16 * lane;
+            const int sp = P / (8 * UW), wb = P % (8 * UW);
+            const uint32_t src = (uint32_t)__shfl((int)mine, (sp < S ? sp : 0) * LPS) + (uint32_t)wb;
+            uoff[c] = sp < S ? src : 0x80000000u;
+        }
+    }
+    auto ibuf = [&](auto bc) -> uint32_t* {
+        constexpr int bb = decltype(bc)::value;
+        if constexpr (bb == 0) return img0;
+        else if constexpr (bb == 1) return img1;
+        else return img2;
+    };
+    auto dma = [&](auto bc) {
+        uint32_t* I = ibuf(bc);
+#pragma unroll
+        for (int c = 0; c < ND; c++) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)(I + 256 * c), 16, (int)uoff[c], 0, 0, 0);
+            uoff[c] += rowb;
+        }
+    };
+    const int el = 2 * (slot * UW + off + k);
+
+    // window slots: rin[s] = rows the slot's window has summed (-1: idle), jw[s] = its strip row
+    f2 sd[NW];
+    float s12[NW];
+    int rin[NW], jw[NW];
+#pragma unroll
+    for (int s = 0; s < NW; s++) {
+        sd[s] = f2{0.f, 0.f};
+        s12[s] = 0.f;
+        rin[s] = -1;
+        jw[s] = 0;
+    }
+    int nextj = 0;
+    auto finish = [&](int j, f2 sdv, float s12v) {
+        const int gy = yo[r0 + j];
+        const int ipy = (int)floorf((float)(gy * a.pixel_step) * scale - 19.5f);
+        const bool ok = valid && !(ipx < -kWin || ipx >= L.w || ipy < -kWin || ipy >= L.h);
+        const float4 r = lk_A_result(sdv, s12v, ok, a.min_eig);
+        if (valid && k == 0) Ab[(long long)pair * a.npts + gx * a.ny + gy] = r;
+    };
+    // one plane row: its elements (loaded once), then every window that contains it
+    auto row = [&](int t, auto bc) {
+        // row t has landed once only row t + 1's pieces may be outstanding
+        if (t + 1 < R) lk_vmcnt<ND>();
+        else lk_vmcnt0();
+        if (t + 2 < R) dma(std::integral_constant<int, (decltype(bc)::value + 2) % 3>{});
+        __builtin_amdgcn_sched_barrier(0);
+        lds_u2v* lE = (lds_u2v*)(ibuf(bc) + el);
+        uint32_t dw[10];
+#pragma unroll
+        for (int gi = 0; gi < 10; gi++) dw[gi] = lE[4 * gi].x;
+        f2 f[10];
+#pragma unroll
+        for (int gi = 0; gi < 10; gi++) f[gi] = f2{(float)(int16_t)dw[gi], (float)((int)dw[gi] >> 16)};
+        if (nextj < nr && t == nextj * asp) {   // window nextj starts here (slot nextj % NW is free)
+            static_for<0, NW>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                if (nextj % NW == s) {
+                    sd[s] = f2{0.f, 0.f};
+                    s12[s] = 0.f;
+                    rin[s] = 0;
+                    jw[s] = nextj;
+                }
+            });
+            nextj++;
+        }
+        static_for<0, NW>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            if (rin[s] >= 0) {
+#pragma unroll
+                for (int gi = 0; gi < 10; gi++) {
+                    // products exact in float (|Ix|, |Iy| <= 4080): the FMA rounds like k_lk_A's
+                    sd[s] = __builtin_elementwise_fma(f[gi], f[gi], sd[s]);
+                    s12[s] = __builtin_fmaf(f[gi].x, f[gi].y, s12[s]);
+                }
+                if (++rin[s] == kWin) {
+                    finish(jw[s], sd[s], s12[s]);
+                    rin[s] = -1;
+                }
+            }
+        });
+    };
+    dma(std::integral_constant<int, 0>{});
+    if (R > 1) dma(std::integral_constant<int, 1>{});
+#pragma unroll 1
+    for (int t = 0; t < R; t += 3) {
+        row(t, std::integral_constant<int, 0>{});
+        if (t + 1 < R) row(t + 1, std::integral_constant<int, 1>{});
+        if (t + 2 < R) row(t + 2, std::integral_constant<int, 2>{});
+    }
+}
+
 // ---- Newton iterations.  grid: x -> persistent wave (a multiple of 8).  The level's work list
 // is every pair's groups, pair-major; it is cut into 8 contiguous ranges, one per XCD (blocks are
 // dealt to the XCDs round-robin), each with its own queue head.  An XCD's waves thus work on
@@ -969,6 +1140,19 @@ static void launch_A(hipStream_t s, int batch, const LkArgs& a, const uint8_t* c
 }
 
 template <int G, int UW>
+static void launch_A_rows(hipStream_t s, int batch, const LkArgs& a, const uint8_t* cls, float4* Ab, int* qctr, int l)
+{
+    constexpr int S = LkShape<G, UW>::S;
+    const ClassLevel& C = a.plan.lv[l];
+    const int ncg = C.nxp / G;
+    const dim3 grid(((ncg + S - 1) / S) * C.nstrip, batch);
+    if (C.asp >= 10)
+        hipLaunchKernelGGL((k_lk_A_rows<G, UW, 4>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ncg);
+    else
+        hipLaunchKernelGGL((k_lk_A_rows<G, UW, 8>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ncg);
+}
+
+template <int G, int UW>
 static void launch_iter(hipStream_t s, int batch, const LkArgs& a, const uint8_t* cls, const float4* Ab, int* qctr,
                         int l)
 {
@@ -1046,7 +1230,11 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             const int G = C.G, UW = C.UW;
             switch (G * 1000 + UW) {
-#define LK_CASE(g, uw) case g * 1000 + uw: launch_A<g, uw>(sa, nb, b, bcls, bA, bq, l); break;
+#define LK_CASE(g, uw)                                                              \
+    case g * 1000 + uw:                                                             \
+        if (C.asp) launch_A_rows<g, uw>(sa, nb, b, bcls, bA, bq, l);               \
+        else launch_A<g, uw>(sa, nb, b, bcls, bA, bq, l);                          \
+        break;
                 LK_SHAPES
 #undef LK_CASE
             default: return hipErrorInvalidValue;
