@@ -474,17 +474,24 @@ def live_leg(dev, w, h, threads, with_cpu=True, reps=5):
     for _ in range(reps):
         sub = ctx.fit_subspace(traj, 2, 0.5, rng)
     t3 = time.perf_counter()
-    # the node's callback on the resident ring: frames arrive one at a time, alternating a, b
+    # the node's callback on the resident ring: frames arrive one at a time, alternating a, b.  The
+    # node keeps its rgb8 staging frame and its output arrays in page-locked memory, allocated once
+    # (mdx_host_alloc), so the frame upload and the readback are DMA at link rate
+    pinned = os.environ.get("MDX_BENCH_PAGEABLE", "0") == "0"     # (A/B: 1 = pageable host buffers)
+    pa, pb = (mdx.host_empty(a.shape), mdx.host_empty(b.shape)) if pinned else (a.copy(), b.copy())
+    pa[...] = a
+    pb[...] = b
+    pout = ctx.trajectory_buffers(w, h, 5, pinned=pinned)
     ctx.ring_reset()
     for k in range(5):
-        ctx.ring_push(frames[k], 5)
-    rres = ctx.ring_trajectory(w, h, 5)
+        ctx.ring_push(pa if k % 2 == 0 else pb, 5)
+    rres = ctx.ring_trajectory(w, h, 5, out=pout)
     same = bool(np.array_equal(rres.traj.view(np.uint32), res.traj.view(np.uint32)) and
                 rres.num_vectors == res.num_vectors)
     t4 = time.perf_counter()
     for k in range(2 * reps):        # an even count: the ring then holds a b a b a again
-        ctx.ring_push(b if k % 2 == 0 else a, 5)
-        rres = ctx.ring_trajectory(w, h, 5)
+        ctx.ring_push(pb if k % 2 == 0 else pa, 5)
+        rres = ctx.ring_trajectory(w, h, 5, out=pout)
     t5 = time.perf_counter()
     ctx.close()
     out = dict(workload=f"5 x {w}x{h} rgb8 frames, pixel_step 10: node callback on the resident ring "
@@ -495,7 +502,8 @@ def live_leg(dev, w, h, threads, with_cpu=True, reps=5):
                ring_equals_list=same,
                points=int(len(res.traj_len)), complete_trajectories=int(len(traj)),
                outliers=int(sub.is_outlier.sum()),
-               includes="ring: H2D of the new frame + D2H of the outputs; list: H2D of all 5 frames")
+               includes="ring: H2D of the new frame + D2H of the outputs (page-locked host buffers); list: H2D of "
+                        "all 5 frames (pageable)")
     if with_cpu:
         from oracle import pyoracle   # CPU baseline leg only (test infrastructure)
         c0 = time.perf_counter()

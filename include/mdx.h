@@ -274,6 +274,13 @@ int  mdx_fit_subspace(mdx_ctx* ctx, const float* traj, int ntraj, int traj_len, 
                       mdx_rand_state* rng, int* columns, uint8_t* is_outlier, double* residuals,
                       float* outlier_points, int* n_outliers);
 
+/* Page-locked host memory for frames and outputs (e.g. the node's rgb8 staging buffer and its
+ * trajectory outputs): copies between it and the device run as DMA at full link rate, while a
+ * pageable buffer is staged by the runtime through bounce buffers.  Any entry taking host pointers
+ * accepts either.  mdx_host_alloc returns NULL on failure. */
+void* mdx_host_alloc(size_t bytes);
+int mdx_host_free(void* p);
+
 /* Device memory helpers so hosts without a HIP toolchain (ctypes, cgo, JNI) can stage
  * buffers: allocation on the context's device, copies ordered on its stream. */
 void* mdx_dev_alloc(mdx_ctx* ctx, size_t bytes);

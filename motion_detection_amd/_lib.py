@@ -37,6 +37,7 @@ EXPORTED = [
     "mdx_synth_pair", "mdx_debug_copy", "mdx_band_flow_dev", "mdx_band_fit_warp_dev", "mdx_flow_trajectory",
     "mdx_srand", "mdx_rand", "mdx_fit_subspace", "mdx_device_pci", "mdx_build_info",
     "mdx_ring_push", "mdx_ring_trajectory", "mdx_ring_reset", "mdx_input_ready",
+    "mdx_host_alloc", "mdx_host_free",
 ]
 
 # csrc/Makefile STAMPED: the files whose bytes the library's provenance stamp hashes, in order
@@ -136,8 +137,9 @@ def lib() -> C.CDLL:
     L.mdx_build_info.restype = C.c_char_p
     L.mdx_device_sync.argtypes = [vp]
     L.mdx_device_sync.restype = C.c_int
-    L.mdx_input_ready.argtypes = [vp, vp]
-    L.mdx_input_ready.restype = C.c_int
+    if hasattr(L, "mdx_input_ready"):      # (absent from variant builds of older sources: A/B runs)
+        L.mdx_input_ready.argtypes = [vp, vp]
+        L.mdx_input_ready.restype = C.c_int
     L.mdx_flow_warp_diff.argtypes = [vp, u8p, u8p, C.c_int, C.c_int, C.c_int, C.c_int, f32p, u8p, f64p, u8p,
                                      f64p, f64p, C.POINTER(C.c_int)]
     L.mdx_flow_warp_diff.restype = C.c_int
@@ -146,6 +148,11 @@ def lib() -> C.CDLL:
     L.mdx_flow_warp_diff_batch_dev.restype = C.c_int
     L.mdx_warp_diff_dev.argtypes = [vp, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int, C.c_size_t, vp, vp]
     L.mdx_warp_diff_dev.restype = C.c_int
+    if hasattr(L, "mdx_host_alloc"):
+        L.mdx_host_alloc.argtypes = [C.c_size_t]
+        L.mdx_host_alloc.restype = vp
+        L.mdx_host_free.argtypes = [vp]
+        L.mdx_host_free.restype = C.c_int
     L.mdx_dev_alloc.argtypes = [vp, C.c_size_t]
     L.mdx_dev_alloc.restype = vp
     L.mdx_dev_free.argtypes = [vp, vp]

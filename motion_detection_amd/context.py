@@ -175,16 +175,25 @@ class Context:
             fmt = _lib.FMT_GRAY8 if im.ndim == 2 else _lib.FMT_RGB8
         return self._check(lib().mdx_ring_push(self._h, _ptr(im), w, h, im.strides[0], fmt, int(keep)))
 
-    def ring_trajectory(self, w: int, h: int, nimg: int) -> "TrajectoryResult":
-        """calculateOpticalFlowTrajectory over the ring's `nimg` frames (w x h)."""
+    def ring_trajectory(self, w: int, h: int, nimg: int, out: "TrajectoryResult | None" = None) -> "TrajectoryResult":
+        """calculateOpticalFlowTrajectory over the ring's `nimg` frames (w x h).  `out`: arrays to
+        fill (e.g. from trajectory_buffers(pinned=True)), reused across callbacks."""
         n = grid_count(w, h, self.params.pixel_step)
-        traj = np.zeros((n, nimg, 2), np.float32)
-        tlen = np.zeros(n, np.int32)
-        start = np.zeros((n, 2), np.float32)
-        vec = np.zeros((n, 4), np.float64)
+        if out is None:
+            out = self.trajectory_buffers(w, h, nimg)
+        traj, tlen, start, vec = out.traj, out.traj_len, out.start_pts, out.vectors
         num = C.c_int(0)
+        assert traj.shape == (n, nimg, 2) and tlen.shape == (n,) and start.shape == (n, 2) and vec.shape == (n, 4)
         self._check(lib().mdx_ring_trajectory(self._h, _ptr(traj), _ptr(tlen), _ptr(start), _ptr(vec), C.byref(num)))
-        return TrajectoryResult(num.value, traj, tlen, start, vec)
+        out.num_vectors = num.value
+        return out
+
+    def trajectory_buffers(self, w: int, h: int, nimg: int, pinned: bool = False) -> "TrajectoryResult":
+        """Output arrays of a trajectory call; pinned=True puts them in page-locked memory."""
+        n = grid_count(w, h, self.params.pixel_step)
+        mk = (lambda shape, dt: host_empty(shape, dt)) if pinned else (lambda shape, dt: np.zeros(shape, dt))
+        return TrajectoryResult(0, mk((n, nimg, 2), np.float32), mk((n,), np.int32), mk((n, 2), np.float32),
+                                mk((n, 4), np.float64))
 
     def ring_reset(self) -> None:
         self._check(lib().mdx_ring_reset(self._h))
@@ -277,6 +286,39 @@ class Context:
 
     def d2h(self, dst: np.ndarray, src: int):
         self._check(lib().mdx_memcpy_d2h(self._h, _ptr(dst), C.c_void_p(src), dst.nbytes))
+
+
+class _HostBlock:
+    """Owner of one mdx_host_alloc block; freed when the last array viewing it goes away."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = max(1, nbytes)
+        self.ptr = lib().mdx_host_alloc(self.nbytes)
+        if not self.ptr:
+            raise MdxError(f"mdx_host_alloc({nbytes}) failed")
+
+    def __del__(self):
+        try:
+            lib().mdx_host_free(C.c_void_p(self.ptr))
+        except Exception:
+            pass
+
+
+class PinnedArray(np.ndarray):
+    """numpy array over page-locked host memory; views keep the block alive through their base."""
+    _blk = None
+
+
+def host_empty(shape, dtype=np.uint8) -> np.ndarray:
+    """A numpy array in page-locked host memory (include/mdx.h mdx_host_alloc): frames and outputs
+    in it cross PCIe by DMA at full rate.  The block is freed with the array."""
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape)) * dtype.itemsize
+    blk = _HostBlock(n)
+    raw = (C.c_uint8 * blk.nbytes).from_address(blk.ptr)
+    arr = np.frombuffer(raw, dtype=np.uint8, count=n).view(dtype).reshape(shape).view(PinnedArray)
+    arr._blk = blk
+    return arr
 
 
 def synth_pair(seed: int, w: int, h: int, channels: int = 1, nthreads: int = 0):

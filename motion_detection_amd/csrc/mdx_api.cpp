@@ -71,6 +71,7 @@ struct mdx_ctx {
     int ring_cap = 0, ring_w = 0, ring_h = 0, ring_ml = -1;
     bool lk_debug = false;
     bool traj_chain = true;                  // trajectory passes in one launch (MDX_TRAJ_CHAIN=0: per pass)
+    int traj_ppw = 2;                        // trajectory LK points per wave (MDX_TRAJ_PPW: 1 or 2)
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
     int lk_sub = 0;                          // > 0: LK sub-batch cap (MDX_LK_SUB, tests)
@@ -385,6 +386,7 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     if (const char* e = std::getenv("MDX_LK_AROWS")) c->lk_arows = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_TRAJ_CHAIN")) c->traj_chain = std::atoi(e) != 0;
+    if (const char* e = std::getenv("MDX_TRAJ_PPW")) c->traj_ppw = std::atoi(e) == 1 ? 1 : 2;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         g_create_err = "hipStreamCreate failed";
         delete c;
@@ -392,7 +394,13 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     }
     const char* ea = std::getenv("MDX_LK_AUX");
     if (!ea || std::atoi(ea) != 0) {
-        bool ok = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;
+        // MDX_AUX_PRIO=1: the aux stream (class planes, A sums, pipelined front ends) gets the
+        // greatest dispatch priority, so its waves take slots ahead of a persistent iteration launch
+        int least = 0, greatest = 0;
+        const char* ep = std::getenv("MDX_AUX_PRIO");
+        const bool prio = ep && std::atoi(ep) != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess;
+        bool ok = (prio ? hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, greatest)
+                        : hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking)) == hipSuccess;
         for (int i = 0; ok && i <= kMaxLevels + 1; i++)
             ok = hipEventCreateWithFlags(&c->lkev[i], hipEventDisableTiming) == hipSuccess;
         const char* ef = std::getenv("MDX_LK_FLOW");
@@ -952,7 +960,7 @@ static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int
         t.start_pts = c->tstart.as<float>();
         t.num = dnum;
         t.mvs = P.min_vector_size;
-        HIP_OR_RETURN(c, launch_lk_chain(s, a, t));
+        HIP_OR_RETURN(c, launch_lk_chain(s, a, t, c->traj_ppw));
     }
     for (int j = 0; !chain && j + 1 < nimg && npts > 0; j++) {
         LkArgs a{};
@@ -1342,6 +1350,19 @@ extern "C" int mdx_debug_copy(mdx_ctx* c, int which, void* dst, size_t bytes)
     const size_t avail = b.cap - (size_t)(src - static_cast<const uint8_t*>(b.p));
     HIP_OR_RETURN(c, hipMemcpy(dst, src, bytes < avail ? bytes : avail, hipMemcpyDeviceToHost));
     return MDX_OK;
+}
+
+extern "C" void* mdx_host_alloc(size_t bytes)
+{
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
+    return p;
+}
+
+extern "C" int mdx_host_free(void* p)
+{
+    if (!p) return MDX_OK;
+    return hipHostFree(p) == hipSuccess ? MDX_OK : MDX_EHIP;
 }
 
 extern "C" void* mdx_dev_alloc(mdx_ctx* c, size_t bytes)

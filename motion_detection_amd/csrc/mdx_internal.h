@@ -172,7 +172,8 @@ struct TrajChain {
     int* num;                            // [0] num_vectors, [1] hand-off waits that timed out
     double mvs;                          // min_vector_size
 };
-hipError_t launch_lk_chain(hipStream_t s, const LkArgs& a, const TrajChain& t);
+// ppw: points per wave (1: 64 lanes per point, 2: 32 lanes per point)
+hipError_t launch_lk_chain(hipStream_t s, const LkArgs& a, const TrajChain& t, int ppw);
 // Trajectory subspace RANSAC (fitSubspace): mean-subtracted data, nhyp hypotheses of d columns
 // (cols: [nhyp][d]), winner's residuals / outlier flags; best[0] = winner or -1.  Scratch: data
 // [N][2T] floats + 2 (the means), qbuf [nhyp][2T][2T-d] doubles (MDX_SUBSPACE_F32: [nhyp][2T][2T] floats), counts [nhyp].

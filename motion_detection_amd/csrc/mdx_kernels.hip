@@ -473,8 +473,12 @@ typedef short s2k __attribute__((ext_vector_type(2)));
 constexpr int kChainSpinMax = 1 << 19;   // ~0.1 s of s_sleep(8) polls: a lost hand-off gives wrong
                                          // results, never a hung launch
 
+// two points per wave: 144 VGPRs, 3 waves per SIMD (MDX_LK32_WPE=4 squeezes 128 with spills)
+#ifndef MDX_LK32_WPE
+#define MDX_LK32_WPE 1
+#endif
 template <int LPP, bool CHAIN>
-__global__ __launch_bounds__(64) void k_lk(LkArgs a, TrajChain t)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? MDX_LK32_WPE : 1, 8))) void k_lk(LkArgs a, TrajChain t)
 {
     constexpr int WIN = 40, R = 8, NCH = WIN / R, EC = R * WIN / LPP, NE = NCH * EC, PPW = 64 / LPP;
     constexpr int STRIDE = 88;                 // floats per chain (80 used; 4*odd => b128 conflict-free)
@@ -483,13 +487,16 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a, TrajChain t)
     constexpr float FLT_SCALE = 1.f / (1 << 20);
     __shared__ float4 lds4[PPW * PT_FLOATS / 4];
 
-    static_assert(!CHAIN || LPP == 64, "chain mode: one point per wave");
+    static_assert(!CHAIN || LPP == 64 || LPP == 32, "chain mode: one or two points per wave");
+    // row runs: lane s owns RUN adjacent window columns of one row per chunk
+    constexpr int RUN = LPP == 64 ? 5 : LPP == 32 ? 10 : 0;
     const int lane = threadIdx.x;
     const int p = lane / LPP, s = lane % LPP;
-    // chain mode: block b = pass * npts + point (dispatch order: every block a wave waits for was
+    // chain mode: block b = pass * nbp + points (dispatch order: every block a wave waits for was
     // dispatched before it, and pass 0 never waits, so the waits always drain)
-    const int pass = CHAIN ? (int)(blockIdx.x / (unsigned)a.npts) : 0;
-    const int pt = CHAIN ? (int)(blockIdx.x - (unsigned)pass * (unsigned)a.npts) : (int)blockIdx.x * PPW + p;
+    const unsigned nbp = (unsigned)((a.npts + PPW - 1) / PPW);       // blocks per pass
+    const int pass = CHAIN ? (int)(blockIdx.x / nbp) : 0;
+    const int pt = CHAIN ? (int)(blockIdx.x - (unsigned)pass * nbp) * PPW + p : (int)blockIdx.x * PPW + p;
     const int pair = CHAIN ? 0 : blockIdx.y;
     const bool valid = pt < a.npts;
     float* ch = reinterpret_cast<float*>(lds4) + p * PT_FLOATS;
@@ -498,11 +505,11 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a, TrajChain t)
     // element geometry (level independent).  LPP 64: lane s owns a run of 5 adjacent window
     // columns of one row per 8-row chunk (row s >> 3, columns 5 (s & 7) .. +4), so its taps of a
     // chunk are two 12-B row loads (J: v_perm + v_dot2 tap pairs) instead of 4 byte loads per element
-    static_assert(LPP != 64 || EC == 5, "row runs of 5");
+    static_assert(RUN == 0 || EC == RUN, "row runs of RUN columns");
     int woff[EC], ex[EC], ey[EC];
 #pragma unroll
     for (int i = 0; i < EC; i++) {
-        const int e = LPP == 64 ? (s >> 3) * WIN + 5 * (s & 7) + i : s + LPP * i;
+        const int e = RUN ? (s / (WIN / RUN)) * WIN + RUN * (s % (WIN / RUN)) + i : s + LPP * i;
         ey[i] = e / WIN;
         ex[i] = e % WIN;
         woff[i] = (ex[i] & 3) * STRIDE + ey[i] * 10 + (ex[i] >> 2);
@@ -514,6 +521,22 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a, TrajChain t)
         const uint32_t o = (uint32_t)(u & 3);
         lo = __builtin_amdgcn_alignbyte(v.y, v.x, o);
         hi = __builtin_amdgcn_alignbyte(v.z, v.y, o);
+    };
+    // 16 bytes of a row from byte address p, realigned: w[0..2] = bytes p .. p+11 (runs of 10)
+    auto row12 = [](const uint8_t* p, uint32_t (&w)[3]) {
+        const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+        const u4a4k v = *reinterpret_cast<const u4a4k*>(u & ~(uintptr_t)3);
+        const uint32_t o = (uint32_t)(u & 3);
+        w[0] = __builtin_amdgcn_alignbyte(v.y, v.x, o);
+        w[1] = __builtin_amdgcn_alignbyte(v.z, v.y, o);
+        w[2] = __builtin_amdgcn_alignbyte(v.w, v.z, o);
+    };
+    // (byte i, byte i + 1) of a realigned run as a 16-bit pair
+    // (i is a constant once the element loops are unrolled)
+    auto tap_pair = [](const uint32_t (&w)[3], int i) -> s2k {
+        const unsigned sel = 0x0c000c00u | (unsigned)(i & 3) | ((unsigned)((i & 3) + 1) << 16);
+        const uint32_t hi = (i >> 2) + 1 < 3 ? w[(i >> 2) + 1 < 3 ? (i >> 2) + 1 : 2] : 0u;
+        return __builtin_bit_cast(s2k, __builtin_amdgcn_perm(hi, w[i >> 2], sel));
     };
 
     const int gx = valid ? pt / a.ny : 0, gy = valid ? pt % a.ny : 0;
@@ -590,7 +613,25 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a, TrajChain t)
             if (ok) {
                 // LPP 64: the run's I bytes and derivative words of both tap rows, vector loads
                 uint64_t r0 = 0, r1 = 0;
-                uint32_t dr0[6] = {}, dr1[6] = {};
+                uint32_t dr0[RUN == 10 ? 11 : 6] = {}, dr1[RUN == 10 ? 11 : 6] = {};
+                uint32_t i0w[3] = {}, i1w[3] = {};
+                if constexpr (LPP == 32) {
+                    const int o = ibase + c * R * pitch + toff[0];
+                    row12(Ib + o, i0w);
+                    row12(Ib + o + pitch, i1w);
+                    const uint32_t* dp = Db + o;
+#pragma unroll
+                    for (int rr = 0; rr < 2; rr++) {
+                        uint32_t* dr = rr ? dr1 : dr0;
+                        const uint32_t* q = dp + rr * pitch;
+                        const u4a4k a0 = *reinterpret_cast<const u4a4k*>(q);
+                        const u4a4k a1 = *reinterpret_cast<const u4a4k*>(q + 4);
+                        const u3a4k a2 = *reinterpret_cast<const u3a4k*>(q + 8);
+                        dr[0] = a0.x; dr[1] = a0.y; dr[2] = a0.z; dr[3] = a0.w;
+                        dr[4] = a1.x; dr[5] = a1.y; dr[6] = a1.z; dr[7] = a1.w;
+                        dr[8] = a2.x; dr[9] = a2.y; dr[10] = a2.z;
+                    }
+                }
                 if constexpr (LPP == 64) {
                     const int o = ibase + c * R * pitch + toff[0];
                     uint32_t l0, h0, l1, h1;
@@ -614,13 +655,19 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a, TrajChain t)
                     int ival;
                     uint32_t d00, d01, d10, d11;
                     int ixv, iyv;
-                    if constexpr (LPP == 64) {
+                    if constexpr (RUN != 0) {
                         // the same integer sums as below through v_dot2 on 16-bit pairs (tap bytes,
                         // Ix / Iy halves; signed weights), no 32-bit multiplies
                         const s2k W0 = {(short)w00, (short)w01}, W1 = {(short)w10, (short)w11};
-                        const unsigned sel = 0x0c000c00u | (unsigned)i | ((unsigned)(i + 1) << 16);
-                        const s2k t0 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm((uint32_t)(r0 >> 32), (uint32_t)r0, sel));
-                        const s2k t1 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm((uint32_t)(r1 >> 32), (uint32_t)r1, sel));
+                        s2k t0, t1;
+                        if constexpr (LPP == 64) {
+                            const unsigned sel = 0x0c000c00u | (unsigned)i | ((unsigned)(i + 1) << 16);
+                            t0 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm((uint32_t)(r0 >> 32), (uint32_t)r0, sel));
+                            t1 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm((uint32_t)(r1 >> 32), (uint32_t)r1, sel));
+                        } else {
+                            t0 = tap_pair(i0w, i);
+                            t1 = tap_pair(i1w, i);
+                        }
                         ival = __builtin_amdgcn_sdot2(t0, W0, __builtin_amdgcn_sdot2(t1, W1, 256, false), false) >> 9;
                         d00 = dr0[i]; d01 = dr0[i + 1]; d10 = dr1[i]; d11 = dr1[i + 1];
                         const s2k x0 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(d01, d00, 0x05040100u));
@@ -712,20 +759,31 @@ __global__ __launch_bounds__(64) void k_lk(LkArgs a, TrajChain t)
             for (int c = 0; c < NCH; c++) {
                 if (act) {
                     uint32_t j0l = 0, j0h = 0, j1l = 0, j1h = 0;
+                    uint32_t j0w[3] = {}, j1w[3] = {};
                     if constexpr (LPP == 64) {
                         const uint8_t* jp = Jb + (jbase + c * R * pitch + toff[0]);
                         row8(jp, j0l, j0h);
                         row8(jp + pitch, j1l, j1h);
+                    } else if constexpr (LPP == 32) {
+                        const uint8_t* jp = Jb + (jbase + c * R * pitch + toff[0]);
+                        row12(jp, j0w);
+                        row12(jp + pitch, j1w);
                     }
 #pragma unroll
                     for (int i = 0; i < EC; i++) {
                         int jv;
-                        if constexpr (LPP == 64) {
+                        if constexpr (RUN != 0) {
                             // (J[x], J[x+1]) of both tap rows as 16-bit pairs; v_dot2 gives the
                             // reference's int sum j00*v00 + j01*v01 + j10*v10 + j11*v11 exactly
-                            const unsigned sel = 0x0c000c00u | (unsigned)i | ((unsigned)(i + 1) << 16);
-                            const s2k t0 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(j0h, j0l, sel));
-                            const s2k t1 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(j1h, j1l, sel));
+                            s2k t0, t1;
+                            if constexpr (LPP == 64) {
+                                const unsigned sel = 0x0c000c00u | (unsigned)i | ((unsigned)(i + 1) << 16);
+                                t0 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(j0h, j0l, sel));
+                                t1 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(j1h, j1l, sel));
+                            } else {
+                                t0 = tap_pair(j0w, i);
+                                t1 = tap_pair(j1w, i);
+                            }
                             const s2k W0 = {(short)v00, (short)v01}, W1 = {(short)v10, (short)v11};
                             jv = __builtin_amdgcn_sdot2(t0, W0, __builtin_amdgcn_sdot2(t1, W1, 256, false), false) >> 9;
                         } else {
@@ -1512,11 +1570,13 @@ hipError_t launch_traj_init(hipStream_t s, int npts, int ny, int pixel_step, int
     return hipGetLastError();
 }
 
-hipError_t launch_lk_chain(hipStream_t s, const LkArgs& a, const TrajChain& t)
+hipError_t launch_lk_chain(hipStream_t s, const LkArgs& a, const TrajChain& t, int ppw)
 {
-    const long long blocks = (long long)(t.nimg - 1) * a.npts;
-    if (t.nimg < 2 || t.nimg > kMaxTrajImgs || a.npts <= 0 || blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_lk<64, true>), dim3((unsigned)blocks), dim3(64), 0, s, a, t);
+    const long long blocks = (long long)(t.nimg - 1) * ((a.npts + ppw - 1) / ppw);
+    if (t.nimg < 2 || t.nimg > kMaxTrajImgs || a.npts <= 0 || blocks > 0x7fffffffLL || (ppw != 1 && ppw != 2))
+        return hipErrorInvalidValue;
+    if (ppw == 2) hipLaunchKernelGGL((k_lk<32, true>), dim3((unsigned)blocks), dim3(64), 0, s, a, t);
+    else hipLaunchKernelGGL((k_lk<64, true>), dim3((unsigned)blocks), dim3(64), 0, s, a, t);
     return hipGetLastError();
 }
 

@@ -235,6 +235,93 @@ __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t sr
     }
 }
 
+// Fixed-point rows (32/M8 a power of two, i.e. (X0 + M0*x1) * Wd exact).  The reference's
+//   X = cvRound(Wd * fl(X0 + fl(M0*x1)))
+// relative to the staged origin, plus 1/2, is held as a 32-bit fixed-point number
+//   U = [ staged column (8 bits) | fx (5 bits) | fraction (19 bits) ]
+// = A(row, block) + B(x1): A = floor(2^19 (Wd*X0 + 1/2 - 32*sxa)), B = floor(2^19 Wd fl(M0*x1)), so a
+// pixel's coordinates are one 32-bit add per axis and floor(U / 2^19) = X - 32*sxa whenever the
+// fraction of U lies in [1, 2^19 - 3]: the two truncations err by less than 2 units, the double
+// rounding of fl(X0 + t1) by < 2^-17 units, so the true value is in (U - 1, U + 3) and cannot cross
+// an integer (an exact tie, a true fraction of 0, is caught the same way).  Pixels outside that
+// range (about 4 in 2^19) take the reference's FP64 expression.  They are found in two steps: the
+// workgroup's per-axis bucket map marks every fraction of A that any column x1 of a block could
+// turn bad (a row-block whose A falls in a marked bucket carries a flag in s_fx), and only lanes of
+// flagged row-blocks test their four pixels.  Then, per pixel: the tap address is byte 3 of the two
+// sums (one v_perm), the bilinear weight pairs come from fx, fy arithmetically (v_bfe + v_mad_u24:
+// f * 65535 + 32 = (32 - f) | f << 16), and the rest is warp_rows's.
+#ifndef MDX_WARP_EARLY_G
+#define MDX_WARP_EARLY_G 1                    // gray2 loads issued before the footprint wait
+#endif
+constexpr int kBmBits = 13;                   // bucket map: 2^13 buckets of 64 units per axis
+typedef __attribute__((address_space(3))) const v4u lds_u4;
+template <bool ROWCHK>
+__device__ __forceinline__ void warp_rows_fx(lds_u4* fxp, lds_d2* xyp, uint32_t src_base, int nvalid,
+                                             const uint32_t (&G)[kTH / 8], __amdgpu_buffer_rsrc_t mrs, uint32_t moff,
+                                             int ms, const uint32_t (&bx)[4], const uint32_t (&by)[4], double M0,
+                                             double M3, int x1b, double Wd, double mX, double mY, uint32_t bias)
+{
+    // loop constants held in registers once (gfx9 VOP3 takes no literals: otherwise each row would
+    // rematerialise them with v_mov): the gray2 byte selectors in SGPRs, the wx multiplier in a VGPR
+    uint32_t gsel[4], mulx;
+    asm volatile("s_mov_b32 %0, 0x0c000c0c" : "=s"(gsel[0]));
+    asm volatile("s_mov_b32 %0, 0x0c010c0c" : "=s"(gsel[1]));
+    asm volatile("s_mov_b32 %0, 0x0c020c0c" : "=s"(gsel[2]));
+    asm volatile("s_mov_b32 %0, 0x0c030c0c" : "=s"(gsel[3]));
+    asm volatile("v_mov_b32 %0, 0x3fffc0" : "=v"(mulx));    // 64 * 65535
+#pragma unroll
+    for (int i = 0; i < kTH / 8; i++) {
+        const int ri = ROWCHK ? (i < nvalid ? i : 0) : i;
+        const v4u f = fxp[16 * ri];                     // (A_x, A_y, flag) of this lane's row and block
+        uint32_t ux[4], uy[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            ux[k] = f.x + bx[k];
+            uy[k] = f.y + by[k];
+        }
+        if (f.z) {
+            // near a rounding boundary somewhere in this row-block: settle each pixel of this lane
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (((ux[k] & 0x7ffffu) - 1u) > 0x7fffcu || ((uy[k] & 0x7ffffu) - 1u) > 0x7fffcu) {
+                    const d2v xy = xyp[16 * ri];
+                    const double x1 = (double)(x1b + k);
+                    const double ax = xy.x + M0 * x1, ay = xy.y + M3 * x1;
+                    ux[k] = (uint32_t)__double2loint(__builtin_fma(ax, Wd, mX)) << 19;
+                    uy[k] = (uint32_t)__double2loint(__builtin_fma(ay, Wd, mY)) << 19;
+                }
+            }
+        }
+        uint32_t ad[4], wys[4], wxs[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            ad[k] = src_base + __builtin_amdgcn_perm(uy[k], ux[k], 0x0c0c0703u);   // (row << 8) | col
+            const uint32_t fx = __builtin_amdgcn_ubfe(ux[k], 19, 5), fy = __builtin_amdgcn_ubfe(uy[k], 19, 5);
+            wys[k] = __umul24(fy, 65535u) + 32u;               // (32 - fy, fy)
+            wxs[k] = __umul24(fx, mulx) + 2048u;               // 64 * (32 - fx, fx)
+        }
+        uint32_t c0s[4], c1s[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            lds_u8* p = (lds_u8*)(uintptr_t)ad[k];
+            c0s[k] = (uint32_t)p[0] | ((uint32_t)p[1] << 16);
+            c1s[k] = (uint32_t)p[kSP] | ((uint32_t)p[kSP + 1] << 16);
+        }
+        uint32_t e[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u16x2v c0 = __builtin_bit_cast(u16x2v, c0s[k]), c1 = __builtin_bit_cast(u16x2v, c1s[k]);
+            const u16x2v wy = __builtin_bit_cast(u16x2v, wys[k]);
+            const u16x2v q = c0 * wy.xx + c1 * wy.yy;
+            const uint32_t s = __builtin_amdgcn_udot2(q, __builtin_bit_cast(u16x2v, wxs[k]), 32u, false);
+            const uint32_t g16 = __builtin_amdgcn_perm(0u, G[i], gsel[k]);
+            asm("v_sad_u32 %0, %1, %2, %3" : "=v"(e[k]) : "v"(s), "v"(g16), "s"(bias));
+        }
+        const uint32_t out = __builtin_amdgcn_perm(e[1], e[0], 0x0c0c0b09u) | __builtin_amdgcn_perm(e[3], e[2], 0x0b090c0cu);
+        __builtin_amdgcn_raw_buffer_store_b32(out, mrs, (int)moff, i * ms, kCpStream);
+    }
+}
+
 // footprint chunks that cross the image's left / right edge: byte by byte, 0 outside (kept out of
 // line so its per-byte bounds are not computed on the interior path)
 __device__ __noinline__ void stage_edge_chunks(const uint8_t* src, int pitch, int w, int h, int sya, int sx, int ro,
@@ -267,6 +354,9 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[64];             // weight table
     __shared__ __attribute__((aligned(16))) double s_xy[kTH][2][2];         // (X0, Y0) per row, block
     __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
+    __shared__ __attribute__((aligned(16))) uint4 s_fx[kTH][2];             // fixed point: (A_x, A_y, flag)
+    __shared__ __attribute__((aligned(16))) uint32_t s_bm[2][(1 << kBmBits) / 32];   // bucket maps x, y
+    __shared__ __attribute__((aligned(16))) uint32_t s_b[2][kBW];           // B(x1) per axis
     __shared__ TileInfo s_info;
 
     // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs; remap the linear id so
@@ -326,6 +416,10 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     }
 
     // ---- fast path: weight table, per-row X0/Y0 of both blocks, then stage the footprint
+    const double Wd = t.wd;                                  // computed once, by wave 0
+    // 32/M8 a power of two -> (X0 + M0*x1) * Wd is exact: the fixed-point rows (warp_rows_fx)
+    const bool pow2 = Wd != 0.0 && (__double_as_longlong(Wd) & 0x000fffffffffffffLL) == 0;
+    if (pow2 && tid < (1 << kBmBits) / 64) reinterpret_cast<uint4*>(&s_bm[0][0])[tid] = make_uint4(0, 0, 0, 0);
     if (tid < 32) {
         s_tab[2 * tid] = (uint32_t)(32 - tid) | ((uint32_t)tid << 16);
         s_tab[2 * tid + 1] = (uint32_t)(64 * (32 - tid)) | ((uint32_t)(64 * tid) << 16);
@@ -335,6 +429,13 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
         s_xy[r][b][0] = M[0] * xb + M[1] * y + M[2];
         s_xy[r][b][1] = M[3] * xb + M[4] * y + M[5];
     }
+    // gray2: this lane's dwords of its 8 rows, issued before the staging wait so that their latency
+    // overlaps the footprint's (fixed-point path; lanes past the right edge load out of range)
+    const bool col_ok = xs < w;
+    const uint32_t OOB = 0x80000000u;
+    const __amdgpu_buffer_rsrc_t g2rs = buf_rsrc(g2p, (long long)h * g2_pitch);
+    const uint32_t g2off = col_ok ? (uint32_t)((y0 + r0) * g2_pitch + xs) : OOB;
+    uint32_t G[kTH / 8];
     {
         // LDS-DMA (buffer_load ... lds): one wave instruction fills 4 staged rows (lane L -> row
         // 4q + L/16, chunk L%16 at LDS byte 16L of the 1-KiB group), straight from memory to LDS.
@@ -353,7 +454,15 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
             __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, (lds_ptr)&s_src[4 * q * kSP], 16, (int)off, 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_waitcnt(0x0F70);               // vmcnt(0): this wave's DMA has landed
+        if (pow2 && MDX_WARP_EARLY_G) {
+#pragma unroll
+            for (int i = 0; i < kTH / 8; i++)
+                G[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * 8 * g2_pitch, kCpStream);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_waitcnt(0x0F70 | (kTH / 8));   // vmcnt(8): the DMA (issued first) has landed
+        } else {
+            __builtin_amdgcn_s_waitcnt(0x0F70);               // vmcnt(0): this wave's DMA has landed
+        }
         __builtin_amdgcn_sched_barrier(0);
         if (ch < nch && !inner)
             for (int q = wave; 4 * q < t.sh; q += 4) {
@@ -362,44 +471,77 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
             }
     }
     __syncthreads();
+    const double fx_scale = 524288.0;                        // 2^19
+    // floor(v) mod 2^32 for |v| < 2^51: the integer plus 1.5 * 2^52 is exact with ulp 1, so its low
+    // word is the two's-complement low word of floor(v) (a double -> int64 conversion is a
+    // multi-instruction sequence on gfx950)
+    auto floor_lo = [](double v) { return (uint32_t)__double2loint(__builtin_floor(v) + 6755399441055744.0); };
+    if (pow2) {
+        // B(x1) = floor(2^19 Wd fl(M*x1)) per axis and column of a block, into LDS; and the bucket
+        // maps: for column x1, A's fraction is bad iff it lies within -B(x1) - 3 .. -B(x1) + 1
+        // (mod 2^19); mark those fractions' buckets (one or two per column and axis)
+        if (tid < 2 * kBW) {
+            const int ax = tid >> 6, x1 = tid & 63;
+            const double t1 = (ax ? M[3] : M[0]) * (double)x1;
+            const uint32_t B = floor_lo(t1 * (Wd * fx_scale));
+            s_b[ax][x1] = B;
+            const uint32_t lo = (0u - B - 3u) & 0x7ffffu, hi = (0u - B + 1u) & 0x7ffffu;
+            const uint32_t b0 = lo >> (19 - kBmBits), b1 = hi >> (19 - kBmBits);
+            atomicOr(&s_bm[ax][b0 >> 5], 1u << (b0 & 31));
+            atomicOr(&s_bm[ax][b1 >> 5], 1u << (b1 & 31));
+        }
+        __syncthreads();
+        if (tid < 2 * kTH) {
+            const int r = tid >> 1, b = tid & 1;
+            const double vx = Wd * s_xy[r][b][0] + 0.5 - 32.0 * t.sxa, vy = Wd * s_xy[r][b][1] + 0.5 - 32.0 * t.sya;
+            const uint32_t Ax = floor_lo(vx * fx_scale);
+            const uint32_t Ay = floor_lo(vy * fx_scale);
+            const uint32_t bx = (Ax & 0x7ffffu) >> (19 - kBmBits), by = (Ay & 0x7ffffu) >> (19 - kBmBits);
+            const uint32_t flag = ((s_bm[0][bx >> 5] >> (bx & 31)) | (s_bm[1][by >> 5] >> (by & 31))) & 1u;
+            s_fx[r][b] = make_uint4(Ax, Ay, flag, 0u);
+        }
+        __syncthreads();
+    }
 
     // lanes past the right edge compute on a valid column of block 0 and store nothing
-    const bool col_ok = xs < w;
     const int cqe = col_ok ? cq : (cq & 15);
     const int blk = cqe >> 4, x1b = 4 * (cqe & 15);
-    const double Wd = t.wd;                                  // computed once, by wave 0
     const double magic = 6755399441055744.0;                 // 1.5 * 2^52: ulp 1
     const double mX = magic - 32.0 * t.sxa, mY = magic - 32.0 * t.sya;
-    // 32/M8 a power of two -> (X0 + M0*x1) * Wd is exact and fuses with the rounding add
-    const bool pow2 = Wd != 0.0 && (__double_as_longlong(Wd) & 0x000fffffffffffffLL) == 0;
     const int tc = min(max(thresh, -1), 255);                // t < 0: all moving; t >= 255: none
     const uint32_t bias = 0x80000000u - (uint32_t)(65536 * tc + 32800);
-    double tx[4], ty[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        tx[k] = M[0] * (x1b + k);
-        ty[k] = M[3] * (x1b + k);
-        asm volatile("" : "+v"(tx[k]), "+v"(ty[k]));   // keep in registers (no per-row rematerialisation)
-    }
     lds_d2* xyp = (lds_d2*)(&s_xy[r0][blk][0]);
     lds_u8* tabp = (lds_u8*)(&s_tab[0]);
     const uint32_t src_base = (uint32_t)(uintptr_t)(lds_u8*)(&s_src[0]);
     // gray2 rows of this pair; mask rows [0, row1) of the frame (stores past the band drop)
-    const __amdgpu_buffer_rsrc_t g2rs = buf_rsrc(g2p, (long long)h * g2_pitch);
     const __amdgpu_buffer_rsrc_t mrs = buf_rsrc(mp, (long long)row1 * w);
-    const uint32_t OOB = 0x80000000u;
-    const uint32_t g2off = col_ok ? (uint32_t)((y0 + r0) * g2_pitch + xs) : OOB;
     const uint32_t moff = col_ok ? (uint32_t)((y0 + r0) * w + xs) : OOB;
     const int nvalid = (row1 - y0 - r0 + 7) >> 3;            // rows r0 + 8i inside the band: i < nvalid
     const bool rowchk = y0 + kTH > row1;
+    if (pow2 && !MDX_WARP_EARLY_G) {
+#pragma unroll
+        for (int i = 0; i < kTH / 8; i++)
+            G[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * 8 * g2_pitch, kCpStream);
+    }
     if (pow2) {
+        // B(x1) of this lane's four columns (the frame-global per-column half of U)
+        const v4u bxv = *(lds_u4*)(&s_b[0][x1b]), byv = *(lds_u4*)(&s_b[1][x1b]);
+        const uint32_t bx[4] = {bxv.x, bxv.y, bxv.z, bxv.w}, by[4] = {byv.x, byv.y, byv.z, byv.w};
+        lds_u4* fxp = (lds_u4*)(&s_fx[r0][blk]);
         if (!rowchk)
-            warp_rows<true, false>(xyp, tabp, src_base, nvalid, g2rs, g2off, 8 * g2_pitch, mrs, moff, 8 * w, tx, ty, Wd,
-                                   mX, mY, bias);
+            warp_rows_fx<false>(fxp, xyp, src_base, nvalid, G, mrs, moff, 8 * w, bx, by, M[0],
+                                M[3], x1b, Wd, mX, mY, bias);
         else
-            warp_rows<true, true>(xyp, tabp, src_base, nvalid, g2rs, g2off, 8 * g2_pitch, mrs, moff, 8 * w, tx, ty, Wd,
-                                  mX, mY, bias);
+            warp_rows_fx<true>(fxp, xyp, src_base, nvalid, G, mrs, moff, 8 * w, bx, by, M[0],
+                               M[3], x1b, Wd, mX, mY, bias);
     } else {
+        double tx[4], ty[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            tx[k] = M[0] * (x1b + k);
+            ty[k] = M[3] * (x1b + k);
+            asm volatile("" : "+v"(tx[k]), "+v"(ty[k]));   // keep in registers (no per-row rematerialisation)
+        }
         warp_rows<false, true>(xyp, tabp, src_base, nvalid, g2rs, g2off, 8 * g2_pitch, mrs, moff, 8 * w, tx, ty, Wd, mX,
                                mY, bias);
     }
