@@ -56,6 +56,11 @@ struct mdx_ctx {
     int* err_host = nullptr;                 // pinned readback
     int spin_max = kLkSpinDefault;           // MDX_LK_SPIN_MAX (debug: < 0 injects timeouts)
     int lk_cap = 85;                         // MDX_LK_CAP: dataflow launch share of the resident waves (%)
+    // pipelined calls alternate the LK stream parity (MDX_LK_XCALL=1): the next call's first level
+    // then need not queue behind this call's fit / warp.  Measured +0.5% (within noise; the chip is
+    // already saturated by the aux work in that gap), and it moves the LK stage events, so it is off
+    bool lk_xcall = false;
+    int lk_parity = 0;                       // the next pipelined call's LK stream parity
     mdx_params prm{};
     int max_w = 0, max_h = 0, max_batch = 0;
     DevBuf pyr1, pyr2, der, fits;            // pyramid / derivative / fit workspace
@@ -421,6 +426,7 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     }
     if (const char* e = std::getenv("MDX_LK_CAP")) c->lk_cap = std::min(std::max(std::atoi(e), 10), 100);
     if (const char* e = std::getenv("MDX_LK_SPIN_MAX")) c->spin_max = std::atoi(e);
+    if (const char* e = std::getenv("MDX_LK_XCALL")) c->lk_xcall = std::atoi(e) != 0;
     if (ensure(c, c->errw, 16) != MDX_OK || hipMemset(c->errw.p, 0, 16) != hipSuccess ||
         hipHostMalloc((void**)&c->err_host, 16, hipHostMallocDefault) != hipSuccess) {
         g_create_err = "error-word allocation failed";
@@ -612,7 +618,7 @@ static void release_pyr_all(mdx_ctx* c)
 // themselves; otherwise the single kernel, after the Scharr planes unless the caller already
 // computed them (have_scharr).  a: every field but the class-plan ones.
 static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, int h, int gy0, int gy1,
-                  bool have_scharr, hipEvent_t prev_ready = nullptr)
+                  bool have_scharr, hipEvent_t prev_ready = nullptr, int parity = -1, hipEvent_t out_free = nullptr)
 {
     int rc;
     hipStream_t s = c->stream;
@@ -647,15 +653,22 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
         const char* e = std::getenv("MDX_LK_DEBUG_PT");
         a.dbg_pt = e ? std::atoi(e) : -1;
     }
-    // A sums, then the queue heads ([sub-batch][level][XCD]), then the dataflow counters ([level][pair])
+    // A sums, then per parity (parity < 0: no cross-call overlap, parity 0's) the queue heads
+    // ([sub-batch][level][XCD]), the dataflow counters ([level][pair]) and the points carried
+    // between levels ([pair][point]; cross-call overlap only: the next call's coarse levels then
+    // never touch the next_pts this call's classify still reads)
     const size_t abytes = (size_t)g.nlev * batch * npts * sizeof(float4);
     const size_t qbytes = (size_t)batch * kMaxLevels * 8 * kCtrPad * sizeof(int);
-    if ((rc = ensure(c, c->Abuf, abytes + qbytes + (size_t)kMaxLevels * batch * kCtrPad * sizeof(int))) != MDX_OK)
-        return rc;
+    const size_t dbytes = (size_t)kMaxLevels * batch * kCtrPad * sizeof(int);
+    const size_t cbytes = ((size_t)batch * npts * 8 + 127) / 128 * 128;
+    if ((rc = ensure(c, c->Abuf, abytes + 2 * (qbytes + dbytes + cbytes))) != MDX_OK) return rc;
+    const int par = parity < 0 ? 0 : parity;
+    uint8_t* base = c->Abuf.as<uint8_t>() + abytes + par * (qbytes + dbytes + cbytes);
+    a.carry = parity < 0 ? nullptr : reinterpret_cast<float*>(base + qbytes + dbytes);
     HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
-                                  reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes), prev_ready, c->iter2,
-                                  c->flowev, reinterpret_cast<int*>(c->Abuf.as<uint8_t>() + abytes + qbytes),
-                                  c->prm.call_pipelining ? c->lvl_done : nullptr));
+                                  reinterpret_cast<int*>(base), prev_ready, c->iter2, c->flowev,
+                                  reinterpret_cast<int*>(base + qbytes), c->prm.call_pipelining ? c->lvl_done : nullptr,
+                                  par, out_free));
     return MDX_OK;
 }
 
@@ -799,7 +812,17 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         a.eps2 = e * e;
         a.next_pts = d_np;
         a.status = d_st;
-        if ((rc = run_lk(c, g, a, batch, w, h, gy0, gy1, false, prev_ready)) != MDX_OK) return rc;
+        // pipelined calls alternate the LK's stream parity (cross-call overlap: this call's first
+        // level need not wait for the previous call's classify / fit / warp on the context stream);
+        // level 0 waits for the previous call's warp (pyr_free of its half) before writing outputs
+        int parity = -1;
+        hipEvent_t out_free = nullptr;
+        if (pipe && c->lk_xcall) {
+            parity = c->lk_parity;
+            c->lk_parity ^= 1;
+            out_free = c->pyr_free[half ^ 1];
+        }
+        if ((rc = run_lk(c, g, a, batch, w, h, gy0, gy1, false, prev_ready, parity, out_free)) != MDX_OK) return rc;
     }
     mark(c, 4);
     if ((rc = ensure(c, c->csum, classify_scratch_bytes(batch, npts))) != MDX_OK) return rc;

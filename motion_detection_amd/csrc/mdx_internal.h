@@ -102,6 +102,8 @@ struct LkArgs {
     float min_eig;
     double eps2;
     float* next_pts;         // [batch][npts][2]
+    float* carry;            // LK v2: [batch][npts][2] the points carried between levels > 0 (level 0
+                             // reads it, writes next_pts); null: next_pts carries them
     uint8_t* status;         // [batch][npts]
     ClassPlan plan;          // LK v2 only
     const int16_t* cmap;     // [level][axis][128] residue -> class index
@@ -198,9 +200,14 @@ hipError_t launch_traj_update(hipStream_t s, int npts, const float* next_pts, co
 // lvl_done (may be null: calls do not overlap): [kMaxLevels] events, re-recorded after each level's
 // iteration launch; the aux stream waits for the previous call's before rewriting that level's
 // class planes, A sums and queue heads (call pipelining lets the aux stream run a call ahead).
+// Cross-call overlap (call pipelining): parity 1 swaps which of s / s2 carries the even levels, so
+// the next call's first level can start on the other stream while this call's classify / fit / warp
+// run on s; qctr and done must then be the parity's own counters and a.carry non-null, and out_free
+// (the previous call's outputs read) is waited for before level 0 writes next_pts / status.
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
                         float4* Ab, int* qctr, hipEvent_t prev_ready = nullptr, hipStream_t s2 = nullptr,
-                        hipEvent_t* flow_ev = nullptr, int* done = nullptr, hipEvent_t* lvl_done = nullptr);
+                        hipEvent_t* flow_ev = nullptr, int* done = nullptr, hipEvent_t* lvl_done = nullptr,
+                        int parity = 0, hipEvent_t out_free = nullptr);
 // Grid rows [gy0, gy1) only (a row band; others are neither written nor counted).  cand != null:
 // row-band mode -- the band's count and first four accepted points go to *cand (one record per
 // pair) instead of a fit.

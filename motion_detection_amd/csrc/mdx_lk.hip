@@ -778,11 +778,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
             if (a.dbg)
                 a.dbg[((long long)pair * a.g.nlev + level) * a.npts + pt] = make_float4(npx, npy, (float)iters, (float)status);
             const float2 v = make_float2(npx, npy);
+            float* dst = (a.carry && level > 0) ? a.carry : a.next_pts;
             if (a.done)   // read by the next level's launch while this one runs: write-through (sc1)
-                __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.next_pts) + po,
+                __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst) + po,
                                    __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else
-                reinterpret_cast<float2*>(a.next_pts)[po] = v;
+                reinterpret_cast<float2*>(dst)[po] = v;
             if (level == 0) a.status[po] = (uint8_t)status;
         }
         if (a.done && level > 0) {
@@ -857,10 +858,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                             // (wavefront scope: no instruction) keeps the loads below the poll.
                             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                             if (q.valid)
-                                p = __builtin_bit_cast(float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(a.next_pts) + po,
+                                p = __builtin_bit_cast(float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(a.carry ? a.carry : a.next_pts) + po,
                                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                         } else if (q.valid) {
-                            p = reinterpret_cast<const float2*>(a.next_pts)[po];
+                            p = reinterpret_cast<const float2*>(a.carry ? a.carry : a.next_pts)[po];
                         }
                         npx = p.x * 2.f;
                         npy = p.y * 2.f;
@@ -1171,7 +1172,7 @@ static void launch_iter(hipStream_t s, int batch, const LkArgs& a, const uint8_t
 
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
                         float4* Ab, int* qctr, hipEvent_t prev_ready, hipStream_t s2, hipEvent_t* flow_ev, int* done,
-                        hipEvent_t* lvl_done)
+                        hipEvent_t* lvl_done, int parity, hipEvent_t out_free)
 {
     // An XCD range spans at most ceil(n/8) + 1 pairs; its class slabs (and pyramids) must stay
     // addressable by 32-bit buffer offsets, so very large batches of large frames run in
@@ -1180,6 +1181,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
     int sub = batch;
     while (sub > 1 && ((sub + 7) / 8 + 1) * span > 0x7fff0000LL) sub = std::max(1, sub / 2);
     if (a.max_sub > 0) sub = std::max(1, std::min(sub, a.max_sub));   // MDX_LK_SUB (tests), read at mdx_create
+    if (sub < batch) parity = 0;   // sub-batches follow everything on s (their slabs are reused)
     // Class planes and A sums depend on the previous frame only, not on the flow: with an aux
     // stream they run ahead (level L-1's while level L iterates, filling that kernel's tail);
     // every level has its own class planes, A buffer and queue heads, so nothing is overwritten
@@ -1192,6 +1194,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         b.pyr2 = a.pyr2 + (long long)p * a.g.img_bytes;
         b.der = a.der + (long long)p * a.g.der_words;
         b.next_pts = a.next_pts + (long long)p * a.npts * 2;
+        b.carry = a.carry ? a.carry + (long long)p * a.npts * 2 : nullptr;
         b.status = a.status + (long long)p * a.npts;
         if (p) b.dbg = nullptr;   // the trace covers the first sub-batch
         uint8_t* bcls = cls + (long long)p * a.plan.bytes_per_pair;
@@ -1248,19 +1251,28 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         // next level can only start once the whole level is done there, and the dataflow measured
         // 1.5% slower than levels in sequence, so it needs at least two
         const bool flow = aux && s2 && flow_ev && done && a.err && nb % 8 == 0 && nb >= 16 && a.npts % 16 == 0 &&
-                          (reinterpret_cast<uintptr_t>(b.next_pts) & 127) == 0;
+                          (reinterpret_cast<uintptr_t>(b.next_pts) & 127) == 0 &&
+                          (reinterpret_cast<uintptr_t>(b.carry) & 127) == 0;
+        // the even levels' stream (the first level's) and the odd levels'; parity 1 swaps them so
+        // that this call's first level does not queue behind the previous call's fit / warp on s
+        const bool swap = flow && parity && b.carry;
+        hipStream_t s0 = swap ? s2 : s, s1 = swap ? s : s2;
         if (flow) {
-            if (hipError_t e = hipMemsetAsync(done, 0, sizeof(int) * kMaxLevels * nb * kCtrPad, s)) return e;
-            if (hipError_t e = hipEventRecord(flow_ev[0], s)) return e;   // counters zeroed, front end done
-            if (hipError_t e = hipStreamWaitEvent(s2, flow_ev[0], 0)) return e;
+            if (hipError_t e = hipMemsetAsync(done, 0, sizeof(int) * kMaxLevels * nb * kCtrPad, s0)) return e;
+            if (hipError_t e = hipEventRecord(flow_ev[0], s0)) return e;   // counters zeroed, front end done
+            if (hipError_t e = hipStreamWaitEvent(s1, flow_ev[0], 0)) return e;
         }
         for (int l = a.maxl; l >= 0; l--) {
             const ClassLevel& C = a.plan.lv[l];
             // levels alternate between the two streams: level l-1 is enqueued behind level l+1
             // only, so it starts as level l's waves leave
-            hipStream_t st = flow && ((a.maxl - l) & 1) ? s2 : s;
+            hipStream_t st = flow && ((a.maxl - l) & 1) ? s1 : s0;
             if (aux) {
                 if (hipError_t e = hipStreamWaitEvent(st, ev[l], 0)) return e;
+            }
+            // level 0 writes next_pts / status: the previous call's readers of them come first
+            if (l == 0 && out_free) {
+                if (hipError_t e = hipStreamWaitEvent(st, out_free, 0)) return e;
             }
             LkArgs bl = b;
             bl.done = flow ? done : nullptr;
