@@ -688,13 +688,31 @@ def main():
         launch_ms = rs["warp_diff"] / max(rs["calls"], 1)
         alg_bytes = 3.0 * RB * rw * rh     # read gray1 + read gray2 + write mask, 1 B/px each
         achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
+        # the memory ceiling of this access mix: the same 3 B/px as one linear non-temporal pass
+        # (mdx_probe_stream3_dev, same buffers, same event bracketing)
+        for _ in range(2):
+            rctx.probe_stream3_dev(RB * rw * rh, e1, e2, eM)
+        rctx.device_sync()
+        rctx.enable_timing(True)
+        for _ in range(args.steps):
+            rctx.probe_stream3_dev(RB * rw * rh, e1, e2, eM)
+        rctx.device_sync()
+        cs = rctx.stage_ms()
+        copy_ms = cs["warp_diff"] / max(cs["calls"], 1)
+        copy_gbs = alg_bytes / (copy_ms * 1e-3) / 1e9
         pmc = stamped_pmc(args.pmc_json, "config", f"{rw}x{rh}x{RB}")
         traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        kt = stamped_pmc(os.path.join(ROOT, "profiles", "warp_kernel_trace.json"), "config", f"{rw}x{rh}x{RB}")
         roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, kernel="k_warp_diff",
                     workload=f"{rw}x{rh} gray, {RB} pairs per launch, true H (affine), 3 B/px algorithmic",
                     avg_launch_us=round(launch_ms * 1e3, 2), algorithmic_bytes_per_launch=int(alg_bytes),
-                    read_frac=round((2.0 / 3.0) * achieved / HBM_PEAK_GBS, 4))
+                    copy_ceiling=dict(achieved=round(copy_gbs, 1), avg_launch_us=round(copy_ms * 1e3, 2),
+                                      what="linear 3 B/px pass, 16 B/lane, non-temporal (k_stream3)"),
+                    copy_ceiling_frac=round(copy_gbs / HBM_PEAK_GBS, 4),
+                    frac_of_copy_ceiling=round(achieved / copy_gbs, 4),
+                    kernel_trace=({k: kt[k] for k in ("k_warp_diff", "k_stream3", "frac_of_copy_ceiling",
+                                                       "source") if k in kt} if kt else None))
         for p in (e1, e2, eH, eM):
             rctx.dev_free(p)
         rctx.close()

@@ -301,6 +301,14 @@ int mdx_stage_ms(mdx_ctx* ctx, int stage, float* ms);
  * point) float4 LK gradient sums; 1: per-level LK trace when MDX_LK_DEBUG=1 at create). */
 int mdx_debug_copy(mdx_ctx* ctx, int which, void* dst, size_t bytes);
 
+/* Measurement probe, no reference counterpart: the memory ceiling of k_warp_diff's access mix.
+ * d_mask[i] = |d_a[i] - d_b[i]| > thresh ? 255 : 0 over n bytes (n a multiple of 16, pointers
+ * 16-byte aligned): the same 3 B/px (read two frames, write the mask) as a linear streaming pass,
+ * 16 B per lane, non-temporal.  Queued on the context's stream and timed as its warp_diff stage
+ * (mdx_stage_ms) when timing is on; bench.py reports its rate as roofline.copy_ceiling. */
+int mdx_probe_stream3_dev(mdx_ctx* ctx, size_t n, const uint8_t* d_a, const uint8_t* d_b, uint8_t* d_mask,
+                          int thresh);
+
 /*
  * Synthetic frame-pair generator used by the benchmark and tests (host, deterministic,
  * byte-identical on every x86-64 host).  Spec in DESIGN.md §5: blurred value noise +

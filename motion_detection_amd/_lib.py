@@ -37,7 +37,7 @@ EXPORTED = [
     "mdx_synth_pair", "mdx_debug_copy", "mdx_band_flow_dev", "mdx_band_fit_warp_dev", "mdx_flow_trajectory",
     "mdx_srand", "mdx_rand", "mdx_fit_subspace", "mdx_device_pci", "mdx_build_info",
     "mdx_ring_push", "mdx_ring_trajectory", "mdx_ring_reset", "mdx_input_ready",
-    "mdx_host_alloc", "mdx_host_free",
+    "mdx_host_alloc", "mdx_host_free", "mdx_probe_stream3_dev",
 ]
 
 # csrc/Makefile STAMPED: the files whose bytes the library's provenance stamp hashes, in order
@@ -153,6 +153,9 @@ def lib() -> C.CDLL:
         L.mdx_host_alloc.restype = vp
         L.mdx_host_free.argtypes = [vp]
         L.mdx_host_free.restype = C.c_int
+    if hasattr(L, "mdx_probe_stream3_dev"):
+        L.mdx_probe_stream3_dev.argtypes = [vp, C.c_size_t, vp, vp, vp, C.c_int]
+        L.mdx_probe_stream3_dev.restype = C.c_int
     L.mdx_dev_alloc.argtypes = [vp, C.c_size_t]
     L.mdx_dev_alloc.restype = vp
     L.mdx_dev_free.argtypes = [vp, vp]

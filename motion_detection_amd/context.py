@@ -229,6 +229,11 @@ class Context:
         return self._check(lib().mdx_warp_diff_dev(self._h, batch, C.c_void_p(d_gray1), C.c_void_p(d_gray2), w, h,
                                                    stride, frame_stride, C.c_void_p(d_H), C.c_void_p(d_mask)))
 
+    def probe_stream3_dev(self, n: int, d_a: int, d_b: int, d_mask: int, thresh: int = 190) -> int:
+        """Memory-ceiling probe of k_warp_diff's 3 B/px access mix (include/mdx.h)."""
+        return self._check(lib().mdx_probe_stream3_dev(self._h, n, C.c_void_p(d_a), C.c_void_p(d_b),
+                                                       C.c_void_p(d_mask), thresh))
+
     # -- row-tiled path (one pair split by rows over ranks; include/mdx.h mdx_band_*)
     def band_flow_dev(self, d_img1: int, d_img2: int, w: int, h: int, stride: int, fmt: int, y0: int, y1: int,
                       d_next_pts: int, d_status: int, d_cand: int, d_vectors: int = 0) -> int:

@@ -1300,6 +1300,19 @@ extern "C" int mdx_warp_diff_dev(mdx_ctx* c, int batch, const uint8_t* d_gray1, 
     return MDX_OK;
 }
 
+extern "C" int mdx_probe_stream3_dev(mdx_ctx* c, size_t n, const uint8_t* d_a, const uint8_t* d_b, uint8_t* d_mask,
+                                     int thresh)
+{
+    if (!c) return MDX_EINVAL;
+    if (!d_a || !d_b || !d_mask || n == 0 || n % 16 || ((uintptr_t)d_a | (uintptr_t)d_b | (uintptr_t)d_mask) % 16)
+        return set_err(c, MDX_EINVAL, "mdx_probe_stream3_dev: bad argument");
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    for (int i = 0; i < 6; i++) mark(c, i);
+    HIP_OR_RETURN(c, launch_stream3(c->stream, n, d_a, d_b, d_mask, thresh));
+    mark(c, 6);
+    return MDX_OK;
+}
+
 extern "C" int mdx_band_flow_dev(mdx_ctx* c, const uint8_t* d_img1, const uint8_t* d_img2, int w, int h, int stride,
                                  int fmt, int y0, int y1, float* d_next_pts, uint8_t* d_status, double* d_vectors,
                                  mdx_band_cand* d_cand)

@@ -564,4 +564,34 @@ hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long lo
     return hipGetLastError();
 }
 
+// Memory-ceiling probe (mdx_probe_stream3_dev): k_warp_diff's 3 B/px with no warp -- two frames
+// read and one mask written linearly, 16 B per lane, non-temporal like the kernel's gray2 / mask.
+__global__ __launch_bounds__(256) void k_stream3(const v4u* __restrict__ a, const v4u* __restrict__ b,
+                                                  v4u* __restrict__ o, size_t n16, int t)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n16) return;
+    const v4u x = __builtin_nontemporal_load(a + i), y = __builtin_nontemporal_load(b + i);
+    v4u r;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        unsigned m = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int d = (int)((x[k] >> (8 * j)) & 255u) - (int)((y[k] >> (8 * j)) & 255u);
+            m |= ((d > t || -d > t) ? 255u : 0u) << (8 * j);
+        }
+        r[k] = m;
+    }
+    __builtin_nontemporal_store(r, o + i);
+}
+
+hipError_t launch_stream3(hipStream_t s, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* o, int thresh)
+{
+    const size_t n16 = n / 16;
+    hipLaunchKernelGGL(k_stream3, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, s, (const v4u*)a,
+                       (const v4u*)b, (v4u*)o, n16, thresh);
+    return hipGetLastError();
+}
+
 }  // namespace mdx

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 evidence on the GPU box (repo root), HEAD's library.  Two parts so each fits one gpurun call:
 #   bash scripts/r04_collect.sh a   -> GPU tests, default bench, kernel-trace summary of the bench
-#   bash scripts/r04_collect.sh b   -> LK / step / warp PMC passes, LK tail stamps, live-leg kernel
+#   bash scripts/r04_collect.sh b   -> LK / step / warp PMC passes, warp kernel trace, LK tail stamps, live-leg kernel
 #                                      trace, C4 runs
 # Outputs under gpurun_out/r04/; the *_to_json scripts turn them into profiles/ (CPU side).
 set -o pipefail
@@ -26,6 +26,10 @@ else
     step pmc_warp
     BENCH_ARGS="--only-roofline --steps 3 --warmup 1 --no-cpu" \
         bash scripts/pmc_sets.sh warp "FETCH_SIZE" "WRITE_SIZE" > $out/pmc_warp.log 2>&1 || exit 1
+    step warp_kt
+    mkdir -p $out/warp_kt
+    timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $out/warp_kt -o run --output-format csv -- python3 bench.py \
+        --only-roofline --steps 20 --warmup 3 --no-cpu > $out/warp_kt/p1.json 2> $out/warp_kt/p1.err || exit 1
     step lk_tail
     MDX_LK_DEBUG=1 timeout -k 10 200 python3 scripts/lk_tail.py > $out/lk_tail.txt 2> $out/lk_tail.err || exit 1
     step live_kt

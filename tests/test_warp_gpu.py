@@ -103,3 +103,27 @@ def test_warp_4k_true_h(mdx, wctx, oracle):
     w, h = 3840, 2160
     a, b, Ht = mdx.synth_pair(20141105, w, h, 1)
     _run(mdx, wctx, oracle, a[None], b[None], [Ht], 190)
+
+
+def test_copy_ceiling_probe(mdx, wctx):
+    """The bench's copy-ceiling probe (mdx_probe_stream3_dev) computes the same 3 B/px result as an
+    identity warp would: mask = |a - b| > t; and rejects unaligned sizes."""
+    rng = np.random.default_rng(5)
+    n = 1 << 20
+    a = rng.integers(0, 256, n, dtype=np.uint8)
+    b = rng.integers(0, 256, n, dtype=np.uint8)
+    da, db, dm = (wctx.dev_alloc(n) for _ in range(3))
+    try:
+        wctx.h2d(da, a); wctx.h2d(db, b)
+        for t in (-1, 0, 190, 255):
+            wctx.probe_stream3_dev(n, da, db, dm, t)
+            wctx.sync()
+            out = np.empty(n, np.uint8)
+            wctx.d2h(out, dm)
+            ref = np.where(np.abs(a.astype(np.int16) - b.astype(np.int16)) > t, 255, 0).astype(np.uint8)
+            assert np.array_equal(out, ref), t
+        with pytest.raises(mdx.MdxError):
+            wctx.probe_stream3_dev(n - 8, da, db, dm)
+    finally:
+        for p in (da, db, dm):
+            wctx.dev_free(p)
