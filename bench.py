@@ -165,8 +165,8 @@ def cpu_baseline(uniq, w, h, seconds: float, threads: int, simd: bool = True):
 def check_outputs(uniq, outs, B, w, h, ps, threads):
     """Untimed checker (test infrastructure, like cpu_baseline): the oracle's results for the
     `unique` distinct pairs, compared bit for bit with every one of the B slots of the last timed
-    step (slot i holds pair i % unique): next_pts (float32 bits), status, H (float64 bits), mask and
-    num_vectors.  Returns the counts; a mismatch is reported in the line, never hidden."""
+    step (slot i holds pair i % unique): next_pts (float32 bits), status, Vec4d (float64 bits), H
+    (float64 bits), mask and num_vectors.  Returns the counts; a mismatch is reported in the line, never hidden."""
     from oracle import pyoracle
     pyoracle.build()
     refs = [pyoracle.calculate_optical_flow(a, b, nthreads=threads, pixel_step=ps, min_vector_size=1.0, simd=True)
@@ -181,6 +181,8 @@ def check_outputs(uniq, outs, B, w, h, ps, threads):
             diffs.append("status")
         if not np.array_equal(outs["np"][i].view(np.uint32), r["next_pts"].view(np.uint32)):
             diffs.append("next_pts")
+        if not np.array_equal(outs["vec"][i].view(np.uint64), np.asarray(r["vectors"], np.float64).reshape(-1, 4).view(np.uint64)):
+            diffs.append("vectors")
         if not np.array_equal(outs["H"][i].view(np.uint64), r["H"].ravel().view(np.uint64)):
             diffs.append("H")
         if not np.array_equal(outs["mask"][i], r["mask"]):
@@ -188,7 +190,7 @@ def check_outputs(uniq, outs, B, w, h, ps, threads):
         if diffs:
             bad.append({"slot": i, "differs": diffs})
     return dict(checked_pairs=B, distinct_pairs=len(refs), mismatched_pairs=len(bad), mismatches=bad[:8],
-                compared="next_pts bits, status, H bits, mask, num_vectors vs oracle/ (untimed)")
+                compared="next_pts bits, status, Vec4d bits, H bits, mask, num_vectors vs oracle/ (untimed)")
 
 
 REHEARSE = False   # --rehearse: ranks beyond the visible devices may share device 0
@@ -582,15 +584,15 @@ def main():
     devs = gather_devices(D, ctx)
     n = mdx.grid_count(w, h, ps)
     d1, d2 = ctx.dev_alloc(g1.nbytes), ctx.dev_alloc(g2.nbytes)
-    dout = {k: ctx.dev_alloc(sz) for k, sz in dict(np=B * n * 8, st=B * n, mask=B * w * h, H=B * 72,
-                                                      num=B * 4).items()}
+    dout = {k: ctx.dev_alloc(sz) for k, sz in dict(np=B * n * 8, st=B * n, vec=B * n * 32, mask=B * w * h,
+                                                      H=B * 72, num=B * 4).items()}
     ctx.h2d(d1, g1)
     ctx.h2d(d2, g2)
 
     def step():
         ctx.flow_warp_diff_batch_dev(B, d1, d2, w, h, w, w * h, mdx.FMT_GRAY8, d_next_pts=dout["np"],
-                                     d_status=dout["st"], d_mask=dout["mask"], d_H=dout["H"],
-                                     d_num_vectors=dout["num"])
+                                     d_status=dout["st"], d_vectors=dout["vec"], d_mask=dout["mask"],
+                                     d_H=dout["H"], d_num_vectors=dout["num"])
 
     def timed(k):
         """k steps between barriers + device syncs (the device sync also reports an LK hand-off
@@ -619,6 +621,7 @@ def main():
     stages = {k: round(v / calls, 4) for k, v in st.items() if k != "calls"}
     # the last timed step's outputs, checked against the oracle after every timed leg (untimed)
     outs = {k: np.empty(shape, dt) for k, shape, dt in (("np", (B, n, 2), np.float32), ("st", (B, n), np.uint8),
+                                                         ("vec", (B, n, 4), np.float64),
                                                          ("mask", (B, h, w), np.uint8), ("H", (B, 9), np.float64),
                                                          ("num", (B,), np.int32))}
     for k, arr in outs.items():
