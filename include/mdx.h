@@ -241,6 +241,9 @@ int mdx_flow_trajectory(mdx_ctx* ctx, const uint8_t* const* imgs, int nimg, int 
  *   mdx_ring_trajectory  calculateOpticalFlowTrajectory over the frames held (>= 2), outputs exactly
  *                        as mdx_flow_trajectory's (nimg = the ring size).
  *   mdx_ring_reset       empty the ring.
+ * mdx_ring_push only queues the upload and the pyramid on the context's stream: the frame's host
+ * memory (page-locked memory is read by DMA after the call returns) must stay unchanged until the
+ * next mdx_ring_trajectory or mdx_sync returns.
  */
 int mdx_ring_push(mdx_ctx* ctx, const uint8_t* img, int w, int h, int stride, int fmt, int keep);
 int mdx_ring_trajectory(mdx_ctx* ctx, float* traj, int32_t* traj_len, float* start_pts, double* vectors,

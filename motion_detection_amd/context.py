@@ -74,6 +74,7 @@ class Context:
         if not h:
             raise MdxError("mdx_create failed: " + lib().mdx_create_error().decode())
         self._h = C.c_void_p(h)
+        self._ring_hold = []    # frames whose asynchronous ring push may still be reading them
 
     # -- lifetime
     def close(self):
@@ -173,7 +174,11 @@ class Context:
         h, w = im.shape[:2]
         if fmt is None:
             fmt = _lib.FMT_GRAY8 if im.ndim == 2 else _lib.FMT_RGB8
-        return self._check(lib().mdx_ring_push(self._h, _ptr(im), w, h, im.strides[0], fmt, int(keep)))
+        n = self._check(lib().mdx_ring_push(self._h, _ptr(im), w, h, im.strides[0], fmt, int(keep)))
+        # the upload is queued, not done (include/mdx.h): hold the frame until the next
+        # ring_trajectory / sync returns
+        self._ring_hold.append(im)
+        return n
 
     def ring_trajectory(self, w: int, h: int, nimg: int, out: "TrajectoryResult | None" = None) -> "TrajectoryResult":
         """calculateOpticalFlowTrajectory over the ring's `nimg` frames (w x h).  `out`: arrays to
@@ -184,7 +189,11 @@ class Context:
         traj, tlen, start, vec = out.traj, out.traj_len, out.start_pts, out.vectors
         num = C.c_int(0)
         assert traj.shape == (n, nimg, 2) and tlen.shape == (n,) and start.shape == (n, 2) and vec.shape == (n, 4)
-        self._check(lib().mdx_ring_trajectory(self._h, _ptr(traj), _ptr(tlen), _ptr(start), _ptr(vec), C.byref(num)))
+        try:
+            self._check(lib().mdx_ring_trajectory(self._h, _ptr(traj), _ptr(tlen), _ptr(start), _ptr(vec),
+                                                  C.byref(num)))
+        finally:
+            self._ring_hold.clear()
         out.num_vectors = num.value
         return out
 
@@ -254,6 +263,7 @@ class Context:
 
     def sync(self):
         self._check(lib().mdx_sync(self._h))
+        self._ring_hold.clear()
 
     def device_sync(self):
         self._check(lib().mdx_device_sync(self._h))

@@ -447,6 +447,8 @@ extern "C" int mdx_destroy(mdx_ctx* c)
     if (!c) return MDX_EINVAL;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->aux) (void)hipStreamSynchronize(c->aux);          // pipelined front ends
+    if (c->iter2) (void)hipStreamSynchronize(c->iter2);
     DevBuf* bufs[] = {&c->pyr1, &c->pyr2, &c->der, &c->fits, &c->in1, &c->in2, &c->np, &c->st,
                       &c->vec, &c->mask, &c->H, &c->Hext, &c->num, &c->bnp, &c->bst,
                       &c->cls, &c->Abuf, &c->ctab, &c->dbg, &c->csum, &c->tin, &c->tcur, &c->tnp, &c->tst,

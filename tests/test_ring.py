@@ -82,3 +82,23 @@ def test_ring_restarts_on_a_new_frame_size(mdx, ctx, oracle):
     ctx.ring_reset()
     with pytest.raises(mdx.MdxError):
         ctx.ring_trajectory(200, 150, 2)                  # empty ring
+
+
+@pytest.mark.gpu
+def test_ring_pushes_in_flight(mdx, ctx, oracle):
+    """Pushes are queued, not done, when mdx_ring_push returns (include/mdx.h): five pushes queued
+    before one trajectory call, then frames pushed from one reused page-locked buffer, rewritten
+    only after the call returns."""
+    w, h = 640, 480
+    frames = sequence(mdx, oracle, w, h, 7, seed=77, channels=3)
+    ctx.ring_reset()
+    for f in frames[:5]:
+        ctx.ring_push(f, 5)
+    _compare(ctx.ring_trajectory(w, h, 5), oracle.flow_trajectory(frames[:5], pixel_step=10, nthreads=8),
+             "five pushes in flight")
+    buf = mdx.host_empty(frames[0].shape)
+    for k in (5, 6):
+        buf[...] = frames[k]
+        ctx.ring_push(buf, 5)
+        _compare(ctx.ring_trajectory(w, h, 5),
+                 oracle.flow_trajectory(frames[k - 4:k + 1], pixel_step=10, nthreads=8), f"pinned push {k}")
