@@ -15,4 +15,4 @@ for set in "$S1" "$S2"; do
     rc=$?; echo "pass $i rc=$rc"
     [ $rc -le 1 ] || exit $rc
 done
-python3 scripts/pmc_lk_to_json.py $out 3 > $out/pmc_lk.json && cat $out/pmc_lk.json
+python3 scripts/pmc_lk_to_json.py $out auto > $out/pmc_lk.json && cat $out/pmc_lk.json

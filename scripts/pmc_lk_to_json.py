@@ -1,5 +1,7 @@
 """Per-step LK counters from scripts/pmc_lk.sh's passes.
-Usage: python scripts/pmc_lk_to_json.py <dir> <steps covered by the run (warmup + timed)>"""
+Usage: python scripts/pmc_lk_to_json.py <dir> [steps covered by the run | auto]
+auto (default): the steps are counted as the 1080p x 32 k_warp_diff launches (one per step; the bench
+also runs its value_unpipelined steps under the profiler)."""
 import csv
 import glob
 import json
@@ -20,17 +22,23 @@ def bench_stamp(d):
                     pass
     return None
 
-d, steps = sys.argv[1], int(sys.argv[2])
+d = sys.argv[1]
+steps_arg = sys.argv[2] if len(sys.argv) > 2 else "auto"
 tot = defaultdict(float)
 per_kernel = defaultdict(lambda: defaultdict(float))
+warp_ids = defaultdict(set)
 for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
+        if "k_warp_diff" in k and int(r["Grid_Size"]) >= 1920 * 1080 * 32 // 64:
+            warp_ids[f].add(r.get("Dispatch_Id") or r.get("Correlation_Id"))
         if "k_lk" not in k:
             continue
         name = k.split("(")[0].split("<")[0].replace("void ", "").replace("mdx::", "")
         tot[r["Counter_Name"]] += float(r["Counter_Value"])
         per_kernel[name][r["Counter_Name"]] += float(r["Counter_Value"])
+# counters come from several passes, each over the same run: steps = launches seen per pass
+steps = int(steps_arg) if steps_arg != "auto" else max(len(v) for v in warp_ids.values())
 bench = json.load(open(f"{d}/p1.json"))
 cfg = bench["config"]
 w, h = (int(x) for x in cfg["frame"].split("x"))
