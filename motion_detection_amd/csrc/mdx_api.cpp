@@ -72,6 +72,7 @@ struct mdx_ctx {
     DevBuf tin, tcur, tnp, tst, ttraj, tlen, tvec, tstart, tnum, tflag;   // trajectory tracking
     DevBuf straj, sdata, sq, scnt, scols, sres, sout, sbest;      // subspace RANSAC
     DevBuf ring_pyr, ring_der, rin;          // resident frame ring (mdx_ring_*)
+    DevBuf wscr;                             // k_warp_prep's per-pair / per-tile tables
     std::vector<int> ring_order;             // held slots, oldest first
     int ring_cap = 0, ring_w = 0, ring_h = 0, ring_ml = -1;
     bool lk_debug = false;
@@ -454,7 +455,7 @@ extern "C" int mdx_destroy(mdx_ctx* c)
                       &c->cls, &c->Abuf, &c->ctab, &c->dbg, &c->csum, &c->tin, &c->tcur, &c->tnp, &c->tst,
                       &c->ttraj, &c->tlen, &c->tvec, &c->tstart, &c->tnum, &c->tflag, &c->straj, &c->sdata, &c->sq,
                       &c->scnt, &c->scols, &c->sres, &c->sout, &c->sbest, &c->ring_pyr, &c->ring_der, &c->rin,
-                      &c->errw};
+                      &c->errw, &c->wscr};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (c->err_host) (void)hipHostFree(c->err_host);
@@ -843,8 +844,10 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
         const Level& L0 = g.lv[0];
         const uint8_t* g1 = pyr1 + L0.img_off + L0.core();
         const uint8_t* g2 = pyr2 + L0.img_off + L0.core();
+        const size_t wsb = warp_scratch_bytes(batch, w, h);
+        if ((rc = ensure(c, c->wscr, wsb)) != MDX_OK) return rc;
         HIP_OR_RETURN(c, launch_warp_diff(s, batch, g1, g.img_bytes, L0.pitch, g2, g.img_bytes, L0.pitch, w, h, fits,
-                                          d_mask, (long long)w * h, P.thresh));
+                                          d_mask, (long long)w * h, P.thresh, c->wscr.p, wsb));
     }
     if (d_H || d_num) HIP_OR_RETURN(c, launch_export_fit(s, batch, fits, d_H, d_num));
     if (pipe) HIP_OR_RETURN(c, hipEventRecord(c->pyr_free[half], s));
@@ -1295,9 +1298,11 @@ extern "C" int mdx_warp_diff_dev(mdx_ctx* c, int batch, const uint8_t* d_gray1, 
     for (int i = 0; i < 5; i++) mark(c, i);
     HIP_OR_RETURN(c, launch_set_fit_external(s, batch, d_H, fits));
     mark(c, 5);
+    const size_t wsb = warp_scratch_bytes(batch, w, h);
+    if ((rc = ensure(c, c->wscr, wsb)) != MDX_OK) return rc;
     HIP_OR_RETURN(c, launch_warp_diff(s, batch, d_gray1, (long long)frame_stride, stride, d_gray2,
                                       (long long)frame_stride, stride, w, h, fits, d_mask, (long long)w * h,
-                                      c->prm.thresh));
+                                      c->prm.thresh, c->wscr.p, wsb));
     mark(c, 6);
     return MDX_OK;
 }
@@ -1364,8 +1369,10 @@ extern "C" int mdx_band_fit_warp_dev(mdx_ctx* c, int nrec, const mdx_band_cand* 
                                       c->band_built[1]));
     const uint8_t* g1 = c->band_pyr1 + L0.img_off + L0.core();
     const uint8_t* g2 = c->band_pyr2 + L0.img_off + L0.core();
+    const size_t wsb = warp_scratch_bytes(1, w, y1 - y0);
+    if (const int erc = ensure(c, c->wscr, wsb); erc != MDX_OK) return erc;
     HIP_OR_RETURN(c, launch_warp_diff(s, 1, g1, g.img_bytes, L0.pitch, g2, g.img_bytes, L0.pitch, w, h, fits, d_mask_band,
-                                      (long long)w * (y1 - y0), c->prm.thresh, y0, y1));
+                                      (long long)w * (y1 - y0), c->prm.thresh, c->wscr.p, wsb, y0, y1));
     if (d_H || d_num_vectors) HIP_OR_RETURN(c, launch_export_fit(s, 1, fits, d_H, d_num_vectors));
     // the band's pyramids have been read: the pipelined call two calls on may overwrite them
     if (c->prm.call_pipelining) HIP_OR_RETURN(c, hipEventRecord(c->pyr_free[c->band_half], s));

@@ -227,10 +227,13 @@ hipError_t launch_gray_rows(hipStream_t s, const uint8_t* img1, int w, int h, in
                             int pitch, const PairFit* fit, int built0 = 0, int built1 = 0);
 hipError_t launch_set_fit_external(hipStream_t s, int batch, const double* H_external, PairFit* fits);
 // Destination rows [row0, row1) of every pair (row1 <= h); mask row y is at mask + (y - row0) * w.
+// scratch: warp_scratch_bytes(batch, w, rows of the band) of device memory for the per-pair and
+// per-tile tables of k_warp_prep (the launch's own; reused by the next launch on the stream)
+size_t warp_scratch_bytes(int batch, int w, int rows);
 hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,
                             const uint8_t* g2, long long g2_stride, int g2_pitch, int w, int h,
-                            const PairFit* fits, uint8_t* mask, long long mask_stride, int thresh, int row0 = 0,
-                            int row1 = -1);
+                            const PairFit* fits, uint8_t* mask, long long mask_stride, int thresh, void* scratch,
+                            size_t scratch_bytes, int row0 = 0, int row1 = -1);
 hipError_t launch_stream3(hipStream_t s, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* o, int thresh);
 hipError_t launch_export_fit(hipStream_t s, int batch, const PairFit* fits, double* H, int* num_vectors);
 

@@ -105,7 +105,8 @@ struct TileInfo {
 };
 
 // Bounds of the tile's taps, from the reference arithmetic at the corners of its (one or two)
-// reference blocks, one corner per lane 0..7; fast = every |X|, |Y| < 2^30 (no clamp, magic
+// reference blocks, one corner per lane of an aligned group of 8 (lane = its index in the group;
+// every lane of the group returns the result); fast = every |X|, |Y| < 2^30 (no clamp, magic
 // rounding exact) and the footprint fits the staging buffer.
 __device__ TileInfo tile_info(const double* M, int x0, int y0, int w, int yend, int lane)
 {
@@ -137,12 +138,11 @@ __device__ TileInfo tile_info(const double* M, int x0, int y0, int w, int yend, 
     }
     TileInfo t;
     t.wd = Wd;
-    t.sxa = __builtin_amdgcn_readfirstlane(sx_lo) & ~15;
-    t.sya = __builtin_amdgcn_readfirstlane(sy_lo);
-    const int sxb = __builtin_amdgcn_readfirstlane(sx_hi), syb = __builtin_amdgcn_readfirstlane(sy_hi);
-    t.sw = sxb - t.sxa + 2;                    // bytes: columns sxa .. sxb + 1
-    t.sh = syb - t.sya + 2;                    // rows sya .. syb + 1
-    t.fast = __builtin_amdgcn_readfirstlane(ok) && t.sw > 0 && t.sh > 0 && t.sw <= kSP && t.sh <= kSH;
+    t.sxa = sx_lo & ~15;
+    t.sya = sy_lo;
+    t.sw = sx_hi - t.sxa + 2;                  // bytes: columns sxa .. sx_hi + 1
+    t.sh = sy_hi - t.sya + 2;                  // rows sya .. sy_hi + 1
+    t.fast = ok && t.sw > 0 && t.sh > 0 && t.sw <= kSP && t.sh <= kSH;
     return t;
 }
 
@@ -250,9 +250,6 @@ __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t sr
 // flagged row-blocks test their four pixels.  Then, per pixel: the tap address is byte 3 of the two
 // sums (one v_perm), the bilinear weight pairs come from fx, fy arithmetically (v_bfe + v_mad_u24:
 // f * 65535 + 32 = (32 - f) | f << 16), and the rest is warp_rows's.
-#ifndef MDX_WARP_EARLY_G
-#define MDX_WARP_EARLY_G 1                    // gray2 loads issued before the footprint wait
-#endif
 constexpr int kBmBits = 13;                   // bucket map: 2^13 buckets of 64 units per axis
 typedef __attribute__((address_space(3))) const v4u lds_u4;
 template <bool ROWCHK>
@@ -341,23 +338,78 @@ __device__ __noinline__ void stage_edge_chunks(const uint8_t* src, int pitch, in
     }
 }
 
+// Per-pair tables of the fixed-point path, made once per launch by k_warp_prep instead of once per
+// tile: B(x1) = floor(2^19 Wd fl(M*x1)) per axis and column of a block, and the bucket maps (for
+// column x1, A's fraction is bad iff it lies within -B(x1) - 3 .. -B(x1) + 1 mod 2^19; the buckets
+// of those fractions are marked, one or two per column and axis).
+struct WarpPrep {
+    uint32_t B[2][kBW];
+    uint32_t bm[2][(1 << kBmBits) / 32];
+};
+
+// floor(v) mod 2^32 for |v| < 2^51: the integer plus 1.5 * 2^52 is exact with ulp 1, so its low word
+// is the two's-complement low word of floor(v) (a double -> int64 conversion is a multi-instruction
+// sequence on gfx950)
+__device__ __forceinline__ uint32_t floor_lo(double v)
+{
+    return (uint32_t)__double2loint(__builtin_floor(v) + 6755399441055744.0);
+}
+
+// grid: x -> 1 + tile groups, y -> pair.  Block 0 of a pair builds its WarpPrep; every other block
+// takes 32 tiles, one aligned group of 8 lanes per tile, and writes their TileInfo.
+__global__ __launch_bounds__(256) void k_warp_prep(const PairFit* __restrict__ fits, int w, int row0, int row1,
+                                                   int nbx, int nby, TileInfo* __restrict__ tinfo,
+                                                   WarpPrep* __restrict__ prep)
+{
+    const int pair = blockIdx.y, tid = threadIdx.x;
+    const PairFit& f = fits[pair];
+    if (f.fit_status != 0) return;
+    double M[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) M[k] = f.Hinv[k];
+    if (blockIdx.x == 0) {
+        __shared__ uint32_t s_bm[2][(1 << kBmBits) / 32];
+        for (int i = tid; i < (1 << kBmBits) / 16; i += 256) (&s_bm[0][0])[i] = 0;
+        __syncthreads();
+        const double Wd = M[8] != 0.0 ? 32.0 / M[8] : 0.0;
+        if (tid < 2 * kBW) {
+            const int ax = tid >> 6, x1 = tid & 63;
+            const double t1 = (ax ? M[3] : M[0]) * (double)x1;
+            const uint32_t B = floor_lo(t1 * (Wd * 524288.0));
+            prep[pair].B[ax][x1] = B;
+            const uint32_t lo = (0u - B - 3u) & 0x7ffffu, hi = (0u - B + 1u) & 0x7ffffu;
+            const uint32_t b0 = lo >> (19 - kBmBits), b1 = hi >> (19 - kBmBits);
+            atomicOr(&s_bm[ax][b0 >> 5], 1u << (b0 & 31));
+            atomicOr(&s_bm[ax][b1 >> 5], 1u << (b1 & 31));
+        }
+        __syncthreads();
+        for (int i = tid; i < (1 << kBmBits) / 16; i += 256) (&prep[pair].bm[0][0])[i] = (&s_bm[0][0])[i];
+        return;
+    }
+    const int tile = (blockIdx.x - 1) * 32 + (tid >> 3);
+    if (tile >= nbx * nby) return;   // whole groups of 8 leave together
+    const int tx = tile % nbx, ty = tile / nbx;
+    const TileInfo t = tile_info(M, tx * kTW, row0 + ty * kTH, w, row1, tid & 7);
+    if ((tid & 7) == 0) tinfo[(long long)pair * (nbx * nby) + tile] = t;
+}
+
 // grid: x -> tile column, y -> tile row of the band [row0, row1), z -> pair.  256 threads; lane l
 // of wave q owns columns x0 + 4*(l & 31) .. +3 of tile rows 2q + (l >> 5) + 8i, i = 0..7.  The
 // reference's blocking depends on the full height only through bw0, and each pixel's arithmetic
-// on (x, y) only, so a band is exactly the full frame's rows.
+// on (x, y) only, so a band is exactly the full frame's rows.  The tile's footprint bounds and
+// the pair's fixed-point tables come from k_warp_prep, so the setup has one barrier: footprint
+// DMA, gray2 loads and the per-row-block table in flight together, then the row loop.
 __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
                                                    const uint8_t* __restrict__ g2, long long g2_stride, int g2_pitch,
                                                    int w, int h, int bw0, const PairFit* __restrict__ fits,
                                                    uint8_t* __restrict__ mask, long long mask_stride, int thresh,
-                                                   int vec_ok, int row0, int row1)
+                                                   int vec_ok, int row0, int row1, const TileInfo* __restrict__ tinfo,
+                                                   const WarpPrep* __restrict__ prep)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_tab[64];             // weight table
+    __shared__ __attribute__((aligned(16))) uint32_t s_tab[64];             // weight table (FP64 rows)
     __shared__ __attribute__((aligned(16))) double s_xy[kTH][2][2];         // (X0, Y0) per row, block
     __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
     __shared__ __attribute__((aligned(16))) uint4 s_fx[kTH][2];             // fixed point: (A_x, A_y, flag)
-    __shared__ __attribute__((aligned(16))) uint32_t s_bm[2][(1 << kBmBits) / 32];   // bucket maps x, y
-    __shared__ __attribute__((aligned(16))) uint32_t s_b[2][kBW];           // B(x1) per axis
-    __shared__ TileInfo s_info;
 
     // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs; remap the linear id so
     // each XCD walks a contiguous run of tiles (row-major).  Horizontally adjacent tiles share the
@@ -396,13 +448,7 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     const bool affine = (M[6] == 0.0) && (M[7] == 0.0);
     // fast path only over dword-aligned rows with reference blocks of 64 (uniform per workgroup)
     const bool try_fast = affine && bw0 == kBW && vec_ok;
-
-    if (try_fast && wave == 0) {
-        const TileInfo t = tile_info(M, x0, y0, w, row1, lane);
-        if (lane == 0) s_info = t;
-    }
-    if (try_fast) __syncthreads();
-    const TileInfo t = s_info;
+    const TileInfo t = tinfo[(long long)pair * (nbx * nby) + tile];   // uniform: scalar loads
     if (!try_fast || !t.fast) {
         // ---- general path: per pixel, global gathers
         const int nx = max(0, min(4, w - xs));
@@ -415,37 +461,32 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
         return;
     }
 
-    // ---- fast path: weight table, per-row X0/Y0 of both blocks, then stage the footprint
-    const double Wd = t.wd;                                  // computed once, by wave 0
+    // ---- fast path
+    const double Wd = t.wd;
     // 32/M8 a power of two -> (X0 + M0*x1) * Wd is exact: the fixed-point rows (warp_rows_fx)
     const bool pow2 = Wd != 0.0 && (__double_as_longlong(Wd) & 0x000fffffffffffffLL) == 0;
-    if (pow2 && tid < (1 << kBmBits) / 64) reinterpret_cast<uint4*>(&s_bm[0][0])[tid] = make_uint4(0, 0, 0, 0);
-    if (tid < 32) {
+    if (!pow2 && tid < 32) {
         s_tab[2 * tid] = (uint32_t)(32 - tid) | ((uint32_t)tid << 16);
         s_tab[2 * tid + 1] = (uint32_t)(64 * (32 - tid)) | ((uint32_t)(64 * tid) << 16);
     }
-    if (tid < 2 * kTH) {
-        const int r = tid >> 1, b = tid & 1, y = y0 + r, xb = x0 + kBW * b;
-        s_xy[r][b][0] = M[0] * xb + M[1] * y + M[2];
-        s_xy[r][b][1] = M[3] * xb + M[4] * y + M[5];
-    }
-    // gray2: this lane's dwords of its 8 rows, issued before the staging wait so that their latency
-    // overlaps the footprint's (fixed-point path; lanes past the right edge load out of range)
     const bool col_ok = xs < w;
     const uint32_t OOB = 0x80000000u;
     const __amdgpu_buffer_rsrc_t g2rs = buf_rsrc(g2p, (long long)h * g2_pitch);
     const uint32_t g2off = col_ok ? (uint32_t)((y0 + r0) * g2_pitch + xs) : OOB;
+    // lanes past the right edge compute on a valid column of block 0 and store nothing
+    const int cqe = col_ok ? cq : (cq & 15);
+    const int blk = cqe >> 4, x1b = 4 * (cqe & 15);
     uint32_t G[kTH / 8];
+    // LDS-DMA (buffer_load ... lds): one wave instruction fills 4 staged rows (lane L -> row
+    // 4q + L/16, chunk L%16 at LDS byte 16L of the 1-KiB group), straight from memory to LDS.
+    // Chunks past the footprint's width, and rows above / below the image, get an out-of-range
+    // offset and land as zeros (BORDER_CONSTANT); chunks crossing the image's left / right edge
+    // are rewritten byte by byte once the DMA has landed.
+    const int nch = (t.sw + 15) >> 4;                 // <= kSP / 16
+    const int ch = lane & 15, sx = t.sxa + 16 * ch;
+    const bool inner = ch < nch && sx >= 0 && sx + 16 <= w;
     {
-        // LDS-DMA (buffer_load ... lds): one wave instruction fills 4 staged rows (lane L -> row
-        // 4q + L/16, chunk L%16 at LDS byte 16L of the 1-KiB group), straight from memory to LDS.
-        // Chunks past the footprint's width, and rows above / below the image, get an
-        // out-of-range offset and land as zeros (BORDER_CONSTANT); chunks crossing the image's
-        // left / right edge are rewritten byte by byte once the DMA has landed.
-        const int nch = (t.sw + 15) >> 4;                 // <= kSP / 16
         const __amdgpu_buffer_rsrc_t srs = buf_rsrc(src, (long long)h * g1_pitch);
-        const int ch = lane & 15, sx = t.sxa + 16 * ch;
-        const bool inner = ch < nch && sx >= 0 && sx + 16 <= w;
         for (int q = wave; 4 * q < t.sh; q += 4) {
             const int r = 4 * q + (lane >> 4);
             const int sy = t.sya + r;
@@ -453,59 +494,47 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
                                                                                   : 0x80000000u;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, (lds_ptr)&s_src[4 * q * kSP], 16, (int)off, 0, 0, 0);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        if (pow2 && MDX_WARP_EARLY_G) {
-#pragma unroll
-            for (int i = 0; i < kTH / 8; i++)
-                G[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * 8 * g2_pitch, kCpStream);
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_waitcnt(0x0F70 | (kTH / 8));   // vmcnt(8): the DMA (issued first) has landed
-        } else {
-            __builtin_amdgcn_s_waitcnt(0x0F70);               // vmcnt(0): this wave's DMA has landed
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (ch < nch && !inner)
-            for (int q = wave; 4 * q < t.sh; q += 4) {
-                const int r = 4 * q + (lane >> 4);
-                if (r < t.sh) stage_edge_chunks(src, g1_pitch, w, h, t.sya, sx, r, t.sh, t.sh, &s_src[16 * ch]);
-            }
     }
-    __syncthreads();
-    const double fx_scale = 524288.0;                        // 2^19
-    // floor(v) mod 2^32 for |v| < 2^51: the integer plus 1.5 * 2^52 is exact with ulp 1, so its low
-    // word is the two's-complement low word of floor(v) (a double -> int64 conversion is a
-    // multi-instruction sequence on gfx950)
-    auto floor_lo = [](double v) { return (uint32_t)__double2loint(__builtin_floor(v) + 6755399441055744.0); };
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t bx[4] = {0, 0, 0, 0}, by[4] = {0, 0, 0, 0};
     if (pow2) {
-        // B(x1) = floor(2^19 Wd fl(M*x1)) per axis and column of a block, into LDS; and the bucket
-        // maps: for column x1, A's fraction is bad iff it lies within -B(x1) - 3 .. -B(x1) + 1
-        // (mod 2^19); mark those fractions' buckets (one or two per column and axis)
-        if (tid < 2 * kBW) {
-            const int ax = tid >> 6, x1 = tid & 63;
-            const double t1 = (ax ? M[3] : M[0]) * (double)x1;
-            const uint32_t B = floor_lo(t1 * (Wd * fx_scale));
-            s_b[ax][x1] = B;
-            const uint32_t lo = (0u - B - 3u) & 0x7ffffu, hi = (0u - B + 1u) & 0x7ffffu;
-            const uint32_t b0 = lo >> (19 - kBmBits), b1 = hi >> (19 - kBmBits);
-            atomicOr(&s_bm[ax][b0 >> 5], 1u << (b0 & 31));
-            atomicOr(&s_bm[ax][b1 >> 5], 1u << (b1 & 31));
-        }
-        __syncthreads();
-        if (tid < 2 * kTH) {
-            const int r = tid >> 1, b = tid & 1;
-            const double vx = Wd * s_xy[r][b][0] + 0.5 - 32.0 * t.sxa, vy = Wd * s_xy[r][b][1] + 0.5 - 32.0 * t.sya;
-            const uint32_t Ax = floor_lo(vx * fx_scale);
-            const uint32_t Ay = floor_lo(vy * fx_scale);
+        // gray2: this lane's dwords of its 8 rows; B(x1) of its four columns (the per-column half of U)
+#pragma unroll
+        for (int i = 0; i < kTH / 8; i++)
+            G[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * 8 * g2_pitch, kCpStream);
+        const v4u bxv = *reinterpret_cast<const v4u*>(&prep[pair].B[0][x1b]);
+        const v4u byv = *reinterpret_cast<const v4u*>(&prep[pair].B[1][x1b]);
+        bx[0] = bxv.x; bx[1] = bxv.y; bx[2] = bxv.z; bx[3] = bxv.w;
+        by[0] = byv.x; by[1] = byv.y; by[2] = byv.z; by[3] = byv.w;
+    }
+    // per row and block: (X0, Y0) for the FP64 forms, and on the fixed-point path A and its flag
+    // (the pair's bucket maps from k_warp_prep, read through L2)
+    if (tid < 2 * kTH) {
+        const int r = tid >> 1, b = tid & 1, y = y0 + r, xb = x0 + kBW * b;
+        const double X0 = M[0] * xb + M[1] * y + M[2];
+        const double Y0 = M[3] * xb + M[4] * y + M[5];
+        s_xy[r][b][0] = X0;
+        s_xy[r][b][1] = Y0;
+        if (pow2) {
+            const double fx_scale = 524288.0;                        // 2^19
+            const uint32_t Ax = floor_lo((Wd * X0 + 0.5 - 32.0 * t.sxa) * fx_scale);
+            const uint32_t Ay = floor_lo((Wd * Y0 + 0.5 - 32.0 * t.sya) * fx_scale);
             const uint32_t bx = (Ax & 0x7ffffu) >> (19 - kBmBits), by = (Ay & 0x7ffffu) >> (19 - kBmBits);
-            const uint32_t flag = ((s_bm[0][bx >> 5] >> (bx & 31)) | (s_bm[1][by >> 5] >> (by & 31))) & 1u;
+            const WarpPrep& P = prep[pair];
+            const uint32_t flag = ((P.bm[0][bx >> 5] >> (bx & 31)) | (P.bm[1][by >> 5] >> (by & 31))) & 1u;
             s_fx[r][b] = make_uint4(Ax, Ay, flag, 0u);
         }
-        __syncthreads();
     }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);               // vmcnt(0): this wave's DMA (and the rest) landed
+    __builtin_amdgcn_sched_barrier(0);
+    if (ch < nch && !inner)
+        for (int q = wave; 4 * q < t.sh; q += 4) {
+            const int r = 4 * q + (lane >> 4);
+            if (r < t.sh) stage_edge_chunks(src, g1_pitch, w, h, t.sya, sx, r, t.sh, t.sh, &s_src[16 * ch]);
+        }
+    __syncthreads();
 
-    // lanes past the right edge compute on a valid column of block 0 and store nothing
-    const int cqe = col_ok ? cq : (cq & 15);
-    const int blk = cqe >> 4, x1b = 4 * (cqe & 15);
     const double magic = 6755399441055744.0;                 // 1.5 * 2^52: ulp 1
     const double mX = magic - 32.0 * t.sxa, mY = magic - 32.0 * t.sya;
     const int tc = min(max(thresh, -1), 255);                // t < 0: all moving; t >= 255: none
@@ -518,15 +547,7 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     const uint32_t moff = col_ok ? (uint32_t)((y0 + r0) * w + xs) : OOB;
     const int nvalid = (row1 - y0 - r0 + 7) >> 3;            // rows r0 + 8i inside the band: i < nvalid
     const bool rowchk = y0 + kTH > row1;
-    if (pow2 && !MDX_WARP_EARLY_G) {
-#pragma unroll
-        for (int i = 0; i < kTH / 8; i++)
-            G[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * 8 * g2_pitch, kCpStream);
-    }
     if (pow2) {
-        // B(x1) of this lane's four columns (the frame-global per-column half of U)
-        const v4u bxv = *(lds_u4*)(&s_b[0][x1b]), byv = *(lds_u4*)(&s_b[1][x1b]);
-        const uint32_t bx[4] = {bxv.x, bxv.y, bxv.z, bxv.w}, by[4] = {byv.x, byv.y, byv.z, byv.w};
         lds_u4* fxp = (lds_u4*)(&s_fx[r0][blk]);
         if (!rowchk)
             warp_rows_fx<false>(fxp, xyp, src_base, nvalid, G, mrs, moff, 8 * w, bx, by, M[0],
@@ -547,20 +568,33 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     }
 }
 
+size_t warp_scratch_bytes(int batch, int w, int rows)
+{
+    const long long tiles = (long long)((w + kTW - 1) / kTW) * ((rows + kTH - 1) / kTH);
+    return (size_t)batch * (sizeof(WarpPrep) + (size_t)tiles * sizeof(TileInfo)) + 256;
+}
+
 hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long long g1_stride, int g1_pitch,
                             const uint8_t* g2, long long g2_stride, int g2_pitch, int w, int h, const PairFit* fits,
-                            uint8_t* mask, long long mask_stride, int thresh, int row0, int row1)
+                            uint8_t* mask, long long mask_stride, int thresh, void* scratch, size_t scratch_bytes,
+                            int row0, int row1)
 {
     if (row1 < 0) row1 = h;
     if (row0 < 0 || row1 > h || row0 >= row1) return hipErrorInvalidValue;
+    if (!scratch || scratch_bytes < warp_scratch_bytes(batch, w, row1 - row0)) return hipErrorInvalidValue;
     const int bh0 = h < 16 ? h : 16;
     const int bw0 = (1024 / bh0) < w ? (1024 / bh0) : w;
     // dword loads of gray2 / stores of the mask need 4-B aligned rows
     const int vec_ok = ((uintptr_t)g2 % 4 == 0) && g2_stride % 4 == 0 && g2_pitch % 4 == 0 &&
                        ((uintptr_t)mask % 4 == 0) && mask_stride % 4 == 0 && w % 4 == 0;
     const dim3 grid((w + kTW - 1) / kTW, (row1 - row0 + kTH - 1) / kTH, batch);
+    const int ntiles = (int)(grid.x * grid.y);
+    WarpPrep* prep = reinterpret_cast<WarpPrep*>((reinterpret_cast<uintptr_t>(scratch) + 255) & ~(uintptr_t)255);
+    TileInfo* tinfo = reinterpret_cast<TileInfo*>(prep + batch);
+    hipLaunchKernelGGL(k_warp_prep, dim3(1 + (ntiles + 31) / 32, batch), dim3(256), 0, s, fits, w, row0, row1,
+                       (int)grid.x, (int)grid.y, tinfo, prep);
     hipLaunchKernelGGL(k_warp_diff, grid, dim3(256), 0, s, g1, g1_stride, g1_pitch, g2, g2_stride, g2_pitch, w, h, bw0,
-                       fits, mask, mask_stride, thresh, vec_ok, row0, row1);
+                       fits, mask, mask_stride, thresh, vec_ok, row0, row1, tinfo, prep);
     return hipGetLastError();
 }
 
