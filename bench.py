@@ -714,8 +714,9 @@ def main():
                                       what="linear 3 B/px pass, 16 B/lane, non-temporal (k_stream3)"),
                     copy_ceiling_frac=round(copy_gbs / HBM_PEAK_GBS, 4),
                     frac_of_copy_ceiling=round(achieved / copy_gbs, 4),
-                    kernel_trace=({k: kt[k] for k in ("k_warp_diff", "k_stream3", "frac_of_copy_ceiling",
-                                                       "source") if k in kt} if kt else None))
+                    kernel_trace=({k: kt[k] for k in ("launch", "k_warp_diff", "k_warp_prep", "k_stream3",
+                                                       "frac_of_copy_ceiling", "source") if k in kt}
+                                  if kt else None))
         for p in (e1, e2, eH, eM):
             rctx.dev_free(p)
         rctx.close()

@@ -29,19 +29,26 @@ d, config = sys.argv[1], sys.argv[2]
 out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_warp_diff.json")
 w, h, b = (int(v) for v in config.split("x"))
 vals = collections.defaultdict(list)
+prep = collections.defaultdict(list)
+prep_threads = ((w // 128) * (h // 64) // 32) * 256 * b        # k_warp_prep of this launch size
 for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
+        # the roofline launches are the large grids (w*h*b/32 threads: 128x64 tiles of 256 threads),
+        # each preceded by its k_warp_prep (per-pair tables and tile bounds), whose bytes count too
+        if "k_warp_prep" in r["Kernel_Name"] and int(r["Grid_Size"]) >= prep_threads:
+            prep[r["Counter_Name"]].append(float(r["Counter_Value"]))
         if "k_warp_diff" not in r["Kernel_Name"]:
             continue
-        # the roofline launches are the large grids (w*h*b/32 threads: 128x64 tiles of 256 threads)
         if int(r["Grid_Size"]) < (w * h * b) // 64:
             continue
         vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-fetch_kib = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
-write_kib = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
+avg = lambda v: sum(v) / len(v) if v else 0.0  # noqa: E731
+fetch_kib = avg(vals["FETCH_SIZE"]) + avg(prep["FETCH_SIZE"])
+write_kib = avg(vals["WRITE_SIZE"]) + avg(prep["WRITE_SIZE"])
 read_b = 2.0 * fetch_kib * 1024
 write_b = write_kib * 1024
-res = dict(kernel="k_warp_diff", config=config, launches=len(vals["FETCH_SIZE"]),
+res = dict(kernel="k_warp_prep + k_warp_diff", config=config, launches=len(vals["FETCH_SIZE"]),
+           prep_launches=len(prep["FETCH_SIZE"]),
            fetch_size_kib=round(fetch_kib, 1), write_size_kib=round(write_kib, 1),
            read_bytes_per_launch=int(read_b), write_bytes_per_launch=int(write_b),
            hbm_bytes_per_launch=int(read_b + write_b), algorithmic_bytes_per_launch=3 * w * h * b,
