@@ -554,6 +554,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
                     n++;
                 }
                 if (n >= kChainSpinMax && s == 0) atomicAdd(t.num + 1, 1);   // reported as an error by the host
+                // the point's load stays below the poll (wavefront scope: no instruction; the load
+                // is sc1 and issues only once the poll has matched)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             const float2 c = __builtin_bit_cast(
                 float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(t.cur) + pt, __ATOMIC_RELAXED,

@@ -10,7 +10,10 @@ ARGS="--steps 2 --warmup 1 --no-cpu --no-roofline --no-live --no-4k --no-lk-roof
 i=0
 for set in "$S1" "$S2"; do
     i=$((i+1))
-    timeout -s KILL 120 rocprofv3 --pmc $set --kernel-trace -d $out/p$i -o run --output-format csv \
+    # MDX_LK_FLOW=0: counter collection serializes kernels, and the level dataflow's gate kernel would
+    # wait for an iteration launch that cannot start before it ends (reported as MDX_EHIP); the
+    # levels-in-sequence schedule runs the same groups and iterations
+    MDX_LK_FLOW=0 timeout -s KILL 120 rocprofv3 --pmc $set --kernel-trace -d $out/p$i -o run --output-format csv \
         -- python3 bench.py $ARGS > $out/p$i.json 2> $out/p$i.err
     rc=$?; echo "pass $i rc=$rc"
     [ $rc -le 1 ] || exit $rc

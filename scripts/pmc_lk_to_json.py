@@ -47,5 +47,7 @@ out = {"kernels": "k_lk_class + k_lk_A + k_lk_iter", "config": f"{w}x{h}x{cfg['b
        "sq_insts_lds_per_step": tot["SQ_INSTS_LDS"] / steps,
        "per_kernel_valu_per_step": {k: v["SQ_INSTS_VALU"] / steps for k, v in per_kernel.items()},
        "counters_per_step": {k: v / steps for k, v in sorted(tot.items())},
-       "source": "scripts/pmc_lk.sh (rocprofv3 --pmc, two passes)", "src_sha256": bench_stamp(d)}
+       "source": "scripts/pmc_lk.sh (rocprofv3 --pmc, two passes; MDX_LK_FLOW=0: counter collection serializes "
+                 "kernels, so the levels run in sequence -- the same groups and iterations)",
+       "src_sha256": bench_stamp(d)}
 print(json.dumps(out, indent=1))

@@ -56,7 +56,8 @@ res = dict(workload=f"{W}x{H} gray, {B} pairs per step, pixel_step 10 (bench.py 
            hbm_read_mb_per_step=round(tot_r / 1e6, 1), hbm_write_mb_per_step=round(tot_w / 1e6, 1),
            hbm_bytes_per_px=round((tot_r + tot_w) / px, 2), algorithmic_bytes_per_px=9.0,
            per_kernel=rows, correction="read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE",
-           source=os.path.basename(os.path.normpath(d)))
+           source=os.path.basename(os.path.normpath(d)),
+           note="collected with MDX_LK_FLOW=0 (counter collection serializes kernels; same work per kernel)")
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: v for k, v in res.items() if k != "per_kernel"}))
 for r in rows[:15]:

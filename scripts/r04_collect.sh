@@ -21,11 +21,14 @@ else
     step pmc_lk
     bash scripts/pmc_lk.sh > $out/pmc_lk.log 2>&1 || exit 1
     step pmc_step
-    BENCH_ARGS="--steps 2 --warmup 1 --no-cpu --no-roofline --no-live --no-4k --no-lk-roofline" \
+    # dataflow off under counter collection (serialized kernels; see scripts/pmc_lk.sh)
+    MDX_LK_FLOW=0 BENCH_ARGS="--steps 2 --warmup 1 --no-cpu --no-roofline --no-live --no-4k --no-lk-roofline" \
         bash scripts/pmc_sets.sh step "FETCH_SIZE" "WRITE_SIZE" > $out/pmc_step.log 2>&1 || exit 1
     step pmc_warp
     BENCH_ARGS="--only-roofline --steps 3 --warmup 1 --no-cpu" \
         bash scripts/pmc_sets.sh warp "FETCH_SIZE" "WRITE_SIZE" > $out/pmc_warp.log 2>&1 || exit 1
+    step pmc_warp_counters
+    bash scripts/pmc_warp.sh gpurun_out/pmc_warpc > $out/pmc_warpc.log 2>&1 || exit 1
     step warp_kt
     mkdir -p $out/warp_kt
     timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $out/warp_kt -o run --output-format csv -- python3 bench.py \
