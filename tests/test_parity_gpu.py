@@ -263,20 +263,24 @@ def test_row_tiled_matches_full(mdx, monkeypatch, w, h, ps, nb, ch, pipe):
     assert int((out["mask"] != full.mask).sum()) == 0
 
 
-def test_full_path_4k_bit_exact(mdx, oracle):
-    """Config C2 (3840x2160, 5 pyramid levels) through the batched device entry, 2 pairs: every
-    output equals the oracle's (the bench's full_path_4k leg runs this path)."""
-    w, h, B = 3840, 2160, 2
-    pairs = [mdx.synth_pair(40 + i, w, h, 1) for i in range(B)]
+@pytest.mark.parametrize("B,uniq,pipe", [(2, 2, 0), (8, 4, 1)])
+def test_full_path_4k_bit_exact(mdx, oracle, B, uniq, pipe):
+    """Config C2 (3840x2160, 5 pyramid levels) through the batched device entry: every output
+    equals the oracle's.  (8, 4, 1) is the bench's full_path_4k leg exactly: 8 slots holding 4
+    distinct pairs, call pipelining on, the same call made twice back to back without a sync."""
+    w, h = 3840, 2160
+    uniq_pairs = [mdx.synth_pair(40 + i, w, h, 1) for i in range(uniq)]
+    pairs = [uniq_pairs[i % uniq] for i in range(B)]
     g1 = np.stack([p[0] for p in pairs]); g2 = np.stack([p[1] for p in pairs])
     n = mdx.grid_count(w, h, 10)
-    with mdx.Context(0, w, h, B, pixel_step=10, min_vector_size=1.0) as c:
+    with mdx.Context(0, w, h, B, pixel_step=10, min_vector_size=1.0, call_pipelining=pipe) as c:
         bufs = [c.dev_alloc(x) for x in (g1.nbytes, g2.nbytes, B * n * 8, B * n, B * n * 32, B * w * h, B * 72, B * 4)]
         try:
             c.h2d(bufs[0], g1); c.h2d(bufs[1], g2)
-            c.flow_warp_diff_batch_dev(B, bufs[0], bufs[1], w, h, w, w * h, mdx.FMT_GRAY8, d_next_pts=bufs[2],
-                                       d_status=bufs[3], d_vectors=bufs[4], d_mask=bufs[5], d_H=bufs[6],
-                                       d_num_vectors=bufs[7])
+            for _ in range(1 + pipe):
+                c.flow_warp_diff_batch_dev(B, bufs[0], bufs[1], w, h, w, w * h, mdx.FMT_GRAY8, d_next_pts=bufs[2],
+                                           d_status=bufs[3], d_vectors=bufs[4], d_mask=bufs[5], d_H=bufs[6],
+                                           d_num_vectors=bufs[7])
             c.sync()
             npts = np.empty((B, n, 2), np.float32); st = np.empty((B, n), np.uint8)
             vec = np.empty((B, n, 4)); mask = np.empty((B, h, w), np.uint8)
@@ -286,8 +290,10 @@ def test_full_path_4k_bit_exact(mdx, oracle):
         finally:
             for p in bufs:
                 c.dev_free(p)
+    refs = [oracle.calculate_optical_flow(a, b, nthreads=16, pixel_step=10, min_vector_size=1.0)
+            for a, b, _ in uniq_pairs]
     for i in range(B):
-        ref = oracle.calculate_optical_flow(g1[i], g2[i], nthreads=16, pixel_step=10, min_vector_size=1.0)
+        ref = refs[i % uniq]
         assert num[i] == ref["num_vectors"]
         np.testing.assert_array_equal(st[i], ref["status"])
         np.testing.assert_array_equal(npts[i].view(np.uint32), ref["next_pts"].view(np.uint32))
