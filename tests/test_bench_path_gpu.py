@@ -72,11 +72,15 @@ def _call(c, batch, d1, d2, o, w, h):
                                d_vectors=o.get("vec", 0), d_mask=o["mask"], d_H=o["H"], d_num_vectors=o["num"])
 
 
-def test_benchmarked_path_1080p_x32_pipelined(mdx, oracle):
+@pytest.mark.parametrize("xcall", ["0", "1"])
+def test_benchmarked_path_1080p_x32_pipelined(mdx, oracle, monkeypatch, xcall):
     """bench.py's timed step, twice back to back on different inputs (16 distinct pairs, 8 per call,
     each in 4 of the 32 slots), call pipelining on, one sync at the end: every pair's next_pts
     (float32 bits), status, H (float64 bits), mask and num_vectors -- and the Vec4d of the second
-    call -- equal the oracle's."""
+    call -- equal the oracle's.  xcall "1": the same with MDX_LK_XCALL=1 (read at mdx_create; off by
+    default), whose consecutive calls alternate the LK streams and counter sets so that one call's
+    level 0 overlaps the next call's coarse levels."""
+    monkeypatch.setenv("MDX_LK_XCALL", xcall)
     seeds_a = [20141105 + i for i in range(8)]
     seeds_b = [20141205 + i for i in range(8)]
     pairs = _pairs(mdx, seeds_a + seeds_b, W, H)
