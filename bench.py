@@ -196,7 +196,9 @@ def check_outputs(uniq, outs, B, w, h, ps, threads):
 REHEARSE = False   # --rehearse: ranks beyond the visible devices may share device 0
 
 
-VALU_PEAK_WAVE_INSTR = 1024 * 2.4e9 / 4   # 1024 SIMDs x 2.4 GHz, one wave64 VALU instruction per 4 cycles
+VALU_PEAK_WAVE_INSTR = 1024 * 2.4e9 / 4   # 1024 SIMDs x 2.4 GHz, one wave64 VALU instruction per 4 cycles (the
+                                          # issue cost of one wave's stream, measured on this op mix)
+VALU_PEAK_WAVE_INSTR_2CYC = 1024 * 2.4e9 / 2   # the SIMD's 2-cycle wave64 rate (MI355X_MICROARCH.md:54, :473)
 LK_VALU_PER_ELEM_ITER = 5   # minimal per window element and Newton iteration: 2 v_dot2 (bilinear J, folded I),
                             # 1 cvt, 1 v_pk_mul_f32 + 1 v_pk_add_f32 (b1, b2 products rounded before the add)
 LK_VALU_PER_ELEM_A = 2      # minimal per element of the gradient sums: 1 v_pk_fma_f32 + 1 v_fma_f32 (A11/A22, A12)
@@ -627,6 +629,7 @@ def main():
     for k, arr in outs.items():
         ctx.d2h(arr, dout[k])
     num = outs["num"]
+    fallbacks = ctx.lk_fallbacks()
     # the same steps with call pipelining off (the line's value_unpipelined)
     value_unpiped = None
     if pipe and not args.only_roofline:
@@ -646,11 +649,17 @@ def main():
         KB = 8
         k1, k2, _, _ = make_batch(kw, kh, KB, min(4, KB), SEED0 + 500 + 1000 * D.rank, threads)
         kctx = open_ctx(D, kw, kh, KB, pixel_step=ps, min_vector_size=1.0, call_pipelining=pipe)
-        f1, f2, fm = kctx.dev_alloc(k1.nbytes), kctx.dev_alloc(k2.nbytes), kctx.dev_alloc(KB * kw * kh)
+        kn = mdx.grid_count(kw, kh, ps)
+        f1, f2 = kctx.dev_alloc(k1.nbytes), kctx.dev_alloc(k2.nbytes)
+        # every output, as the headline step writes them
+        fo = {k: kctx.dev_alloc(sz) for k, sz in dict(np=KB * kn * 8, st=KB * kn, vec=KB * kn * 32,
+                                                      mask=KB * kw * kh, H=KB * 72, num=KB * 4).items()}
         kctx.h2d(f1, k1); kctx.h2d(f2, k2)
 
         def step4k():
-            kctx.flow_warp_diff_batch_dev(KB, f1, f2, kw, kh, kw, kw * kh, mdx.FMT_GRAY8, d_mask=fm)
+            kctx.flow_warp_diff_batch_dev(KB, f1, f2, kw, kh, kw, kw * kh, mdx.FMT_GRAY8, d_next_pts=fo["np"],
+                                          d_status=fo["st"], d_vectors=fo["vec"], d_mask=fo["mask"], d_H=fo["H"],
+                                          d_num_vectors=fo["num"])
 
         for _ in range(max(1, args.warmup)):
             step4k()
@@ -663,8 +672,10 @@ def main():
         D.barrier()
         rate4k, el4k = throughput(D, float(args.steps * KB * kw * kh), time.perf_counter() - t0)
         full4k = dict(workload=f"{kw}x{kh} gray pairs, whole reference path (max_level 5 -> 5 levels)", batch_per_gpu=KB,
-                      value=round(rate4k / 1e6, 2), unit="Mpixels/s", ms_per_step=round(el4k / args.steps * 1e3, 3))
-        for p in (f1, f2, fm):
+                      value=round(rate4k / 1e6, 2), unit="Mpixels/s", ms_per_step=round(el4k / args.steps * 1e3, 3),
+                      outputs="next_pts, status, Vec4d, mask, H, num_vectors (as the headline step)",
+                      lk_fallbacks=kctx.lk_fallbacks())
+        for p in [f1, f2] + list(fo.values()):
             kctx.dev_free(p)
         kctx.close()
         del k1, k2
@@ -745,7 +756,11 @@ def main():
         alg_wave = wk["valu_lane_instr_per_pair"] * B / 64.0
         ach = alg_wave / (stages["lk"] * 1e-3)
         lk_roof = dict(bound="valu", unit="wave-instr/s", achieved=round(ach, 1), peak=VALU_PEAK_WAVE_INSTR,
-                       frac=round(ach / VALU_PEAK_WAVE_INSTR, 4), stage_ms=stages["lk"],
+                       frac=round(ach / VALU_PEAK_WAVE_INSTR, 4),
+                       peak_basis="4 cycles per wave64 VALU instruction (one wave's issue cost, measured op mix)",
+                       peak_2cyc=VALU_PEAK_WAVE_INSTR_2CYC, frac_2cyc=round(ach / VALU_PEAK_WAVE_INSTR_2CYC, 4),
+                       peak_2cyc_basis="2 cycles per wave64 VALU instruction (SIMD rate, MI355X_MICROARCH.md:54)",
+                       stage_ms=stages["lk"],
                        algorithmic_wave_instr_per_step=round(alg_wave, 1), per_element=dict(
                            iteration=LK_VALU_PER_ELEM_ITER, gradient_sums=LK_VALU_PER_ELEM_A),
                        workload=f"{B} pairs {w}x{h}, pixel_step {ps}, {wk['levels']} levels", **{
@@ -788,6 +803,7 @@ def main():
                             "points_per_s": round(px_all / (w * h) * mdx.grid_count(w, h, ps) / el_max, 1),
                             "roofline": lk_roof},
         "num_vectors_pair0": int(num[0]),
+        "lk_fallbacks": fallbacks,
         "full_path_4k": full4k,
         "live_path": live,
     }

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define MDX_ABI_VERSION 2    /* 2: mdx_params.call_pipelining, mdx_input_ready */
+#define MDX_ABI_VERSION 3    /* 2: mdx_params.call_pipelining, mdx_input_ready; 3: mdx_lk_fallbacks */
 
 /* Return codes */
 #define MDX_OK           0
@@ -104,13 +104,21 @@ int mdx_device_pci(const mdx_ctx* ctx, char* buf, int len);
 /* Build provenance: "src_sha256=<sha256 of the library's sources> arch=gfx950", compiled in by
  * csrc/Makefile.  tests/test_abi.py checks it against the sources in the tree. */
 const char* mdx_build_info(void);
-/* Wait for the context's work.  Returns MDX_EHIP if an LK hand-off between pyramid levels timed
- * out in any call since the last check (the LK level dataflow of the batched entry: a group waits,
- * bounded, for its pair's coarser level); the outputs of those calls are then invalid.  A wait
- * that long means the device was preempted or oversubscribed; it is never silent. */
+/* Wait for the context's work (and collect the LK fallback counts below). */
 int mdx_sync(mdx_ctx* ctx);
-/* hipDeviceSynchronize on the context's device (all streams); the same hand-off check. */
+/* hipDeviceSynchronize on the context's device (all streams); the same collection. */
 int mdx_device_sync(mdx_ctx* ctx);
+/* LK level dataflow fallbacks since mdx_create, as of the last mdx_sync / mdx_device_sync:
+ *   counts[0]  group waits that gave up (a group of level l waits, bounded, for its pair's level
+ *              l+1 groups, whose launch may not be dispatched in time: the device is preempted,
+ *              shared, or serializes kernels as a counter-collecting profiler does)
+ *   counts[1]  gate waits that gave up (the same, before a level's launch)
+ *   counts[2]  levels recomputed
+ * A level whose wait gave up is abandoned and recomputed in sequence within the same call, after
+ * its coarser level, together with every finer level: the outputs are exact either way (the
+ * reference call always returns a result, optical_flow_calculator.cpp:71).  The counts are
+ * statistics, not errors. */
+int mdx_lk_fallbacks(const mdx_ctx* ctx, long long counts[3]);
 /* Name the input frames' producer: the next device-entry call (mdx_flow_warp_diff_batch_dev,
  * mdx_band_flow_dev, mdx_warp_diff_dev) makes its first stage wait for `hip_event` (a hipEvent_t
  * the caller recorded on its own stream after writing the frames) before reading them.  One-shot:

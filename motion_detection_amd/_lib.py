@@ -37,7 +37,7 @@ EXPORTED = [
     "mdx_synth_pair", "mdx_debug_copy", "mdx_band_flow_dev", "mdx_band_fit_warp_dev", "mdx_flow_trajectory",
     "mdx_srand", "mdx_rand", "mdx_fit_subspace", "mdx_device_pci", "mdx_build_info",
     "mdx_ring_push", "mdx_ring_trajectory", "mdx_ring_reset", "mdx_input_ready",
-    "mdx_host_alloc", "mdx_host_free", "mdx_probe_stream3_dev",
+    "mdx_host_alloc", "mdx_host_free", "mdx_probe_stream3_dev", "mdx_lk_fallbacks",
 ]
 
 # csrc/Makefile STAMPED: the files whose bytes the library's provenance stamp hashes, in order
@@ -148,6 +148,9 @@ def lib() -> C.CDLL:
     L.mdx_flow_warp_diff_batch_dev.restype = C.c_int
     L.mdx_warp_diff_dev.argtypes = [vp, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int, C.c_size_t, vp, vp]
     L.mdx_warp_diff_dev.restype = C.c_int
+    if hasattr(L, "mdx_lk_fallbacks"):
+        L.mdx_lk_fallbacks.argtypes = [vp, C.POINTER(C.c_longlong)]
+        L.mdx_lk_fallbacks.restype = C.c_int
     if hasattr(L, "mdx_host_alloc"):
         L.mdx_host_alloc.argtypes = [C.c_size_t]
         L.mdx_host_alloc.restype = vp

@@ -189,11 +189,13 @@ class Context:
         traj, tlen, start, vec = out.traj, out.traj_len, out.start_pts, out.vectors
         num = C.c_int(0)
         assert traj.shape == (n, nimg, 2) and tlen.shape == (n,) and start.shape == (n, 2) and vec.shape == (n, 4)
-        try:
-            self._check(lib().mdx_ring_trajectory(self._h, _ptr(traj), _ptr(tlen), _ptr(start), _ptr(vec),
-                                                  C.byref(num)))
-        finally:
-            self._ring_hold.clear()
+        rc = lib().mdx_ring_trajectory(self._h, _ptr(traj), _ptr(tlen), _ptr(start), _ptr(vec), C.byref(num))
+        if rc < 0:
+            # the uploads queued by earlier ring_push calls may still read the held frames: release
+            # them only once the stream has drained
+            lib().mdx_sync(self._h)
+        self._ring_hold.clear()
+        self._check(rc)
         out.num_vectors = num.value
         return out
 
@@ -268,6 +270,13 @@ class Context:
     def device_sync(self):
         self._check(lib().mdx_device_sync(self._h))
 
+    def lk_fallbacks(self) -> dict:
+        """LK level-dataflow fallbacks since creation, as of the last sync (include/mdx.h
+        mdx_lk_fallbacks): waits that gave up and levels recomputed -- statistics, not errors."""
+        v = (C.c_longlong * 3)()
+        self._check(lib().mdx_lk_fallbacks(self._h, v))
+        return {"group_giveups": v[0], "gate_giveups": v[1], "levels_recomputed": v[2]}
+
     @property
     def stream(self) -> int:
         return lib().mdx_stream(self._h) or 0
@@ -331,6 +340,10 @@ def host_empty(shape, dtype=np.uint8) -> np.ndarray:
     n = int(np.prod(shape)) * dtype.itemsize
     blk = _HostBlock(n)
     raw = (C.c_uint8 * blk.nbytes).from_address(blk.ptr)
+    # the block hangs off the lowest buffer object: numpy collapses a view's base chain down to
+    # `raw` (np.asarray, .view(np.ndarray) and ascontiguousarray skip the PinnedArray), so every
+    # view of the memory keeps it alive
+    raw._blk = blk
     arr = np.frombuffer(raw, dtype=np.uint8, count=n).view(dtype).reshape(shape).view(PinnedArray)
     arr._blk = blk
     return arr

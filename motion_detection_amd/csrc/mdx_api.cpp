@@ -39,6 +39,7 @@ struct mdx_ctx {
     hipEvent_t front_ev = nullptr;
     hipEvent_t pyr_free[2] = {};             // on `stream`, after the last reader of each half
     hipEvent_t lvl_done[kMaxLevels] = {};    // the last call's iteration launch of each level
+    hipEvent_t redo_ev[kMaxLevels] = {};     // LK dataflow: each level's launch + recompute done (fallback order)
     int pyr_half = 0;                        // the half the next pipelined call writes
     hipEvent_t input_ev = nullptr;           // mdx_input_ready: the next device call's inputs (caller-owned)
     uint8_t* last_pyr1 = nullptr;            // the last pair call's pyramids (debug copies)
@@ -51,9 +52,11 @@ struct mdx_ctx {
     const uint8_t* band_img1 = nullptr;      // the last mdx_band_flow_dev's frame 1 (its fit/warp reads it)
     int band_built[2] = {0, 0};              // level-0 rows of frame 1 that call's pyramid build wrote
     int band_stride = 0, band_fmt = 0;
-    // LK dataflow hand-off timeouts ([0] group waits, [1] gate waits), read back at the sync points
+    // LK dataflow fallback statistics ([0] group waits and [1] gate waits that gave up, [2] levels
+    // recomputed), read back and cleared at the sync points, accumulated in lk_fallback
     DevBuf errw;
     int* err_host = nullptr;                 // pinned readback
+    long long lk_fallback[3] = {0, 0, 0};
     int spin_max = kLkSpinDefault;           // MDX_LK_SPIN_MAX (debug: < 0 injects timeouts)
     int lk_cap = 85;                         // MDX_LK_CAP: dataflow launch share of the resident waves (%)
     // pipelined calls alternate the LK stream parity (MDX_LK_XCALL=1): the next call's first level
@@ -413,6 +416,8 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
         if (ok && (!ef || std::atoi(ef) != 0)) {
             ok = hipStreamCreateWithFlags(&c->iter2, hipStreamNonBlocking) == hipSuccess;
             for (int i = 0; ok && i < 2; i++) ok = hipEventCreateWithFlags(&c->flowev[i], hipEventDisableTiming) == hipSuccess;
+            for (int i = 0; ok && i < kMaxLevels; i++)
+                ok = hipEventCreateWithFlags(&c->redo_ev[i], hipEventDisableTiming) == hipSuccess;
         }
         // call pipelining's events (mdx_params.call_pipelining may be switched on at any call)
         ok = ok && hipEventCreateWithFlags(&c->front_ev, hipEventDisableTiming) == hipSuccess;
@@ -475,6 +480,8 @@ extern "C" int mdx_destroy(mdx_ctx* c)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->flowev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->redo_ev)
+        if (e) (void)hipEventDestroy(e);
     delete c;
     return MDX_OK;
 }
@@ -504,26 +511,38 @@ extern "C" int mdx_get_params(const mdx_ctx* c, mdx_params* p)
     return MDX_OK;
 }
 
-// The LK dataflow's hand-off timeouts since the last check: queue the error word's readback on the
-// context stream (every LK launch of a call is joined into it), and after the caller's sync
-// lk_err_result turns a nonzero count into MDX_EHIP and clears the word.
+// The LK dataflow's fallbacks since the last check: queue the statistics word's readback on the
+// context stream (every LK launch of a call is joined into it); after the caller's sync
+// lk_err_result adds them to the context's totals (mdx_lk_fallbacks) and clears the word.  A wait
+// that gave up is not an error: its level was recomputed in sequence within the same call.
 static int queue_lk_err(mdx_ctx* c)
 {
-    HIP_OR_RETURN(c, hipMemcpyAsync(c->err_host, c->errw.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OR_RETURN(c, hipMemcpyAsync(c->err_host, c->errw.p, 12, hipMemcpyDeviceToHost, c->stream));
     return MDX_OK;
 }
 
 static int lk_err_result(mdx_ctx* c)
 {
-    const int groups = c->err_host[0], gates = c->err_host[1];
-    if (groups == 0 && gates == 0) return MDX_OK;
-    c->err_host[0] = c->err_host[1] = 0;
-    HIP_OR_RETURN(c, hipMemsetAsync(c->errw.p, 0, 8, c->stream));
+    const int groups = c->err_host[0], gates = c->err_host[1], redone = c->err_host[2];
+    if (groups == 0 && gates == 0 && redone == 0) return MDX_OK;
+    c->err_host[0] = c->err_host[1] = c->err_host[2] = 0;
+    c->lk_fallback[0] += groups;
+    c->lk_fallback[1] += gates;
+    c->lk_fallback[2] += redone;
+    HIP_OR_RETURN(c, hipMemsetAsync(c->errw.p, 0, 12, c->stream));
     HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
-    return set_err(c, MDX_EHIP,
-                   "LK level dataflow: %d group hand-off wait(s) and %d gate wait(s) timed out (device preempted or "
-                   "oversubscribed?); the outputs of the calls since the last sync are invalid",
-                   groups, gates);
+    // a give-up is always followed by its level's recompute (launch_lk_v2): one without it would be
+    // a scheduling bug, and its outputs could be wrong
+    if (groups > 0 && redone == 0)
+        return set_err(c, MDX_EHIP, "LK dataflow: %d wait(s) gave up but no level was recomputed", groups);
+    return MDX_OK;
+}
+
+extern "C" int mdx_lk_fallbacks(const mdx_ctx* c, long long* counts)
+{
+    if (!c || !counts) return MDX_EINVAL;
+    for (int i = 0; i < 3; i++) counts[i] = c->lk_fallback[i];
+    return MDX_OK;
 }
 
 extern "C" int mdx_sync(mdx_ctx* c)
@@ -662,16 +681,18 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
     // never touch the next_pts this call's classify still reads)
     const size_t abytes = (size_t)g.nlev * batch * npts * sizeof(float4);
     const size_t qbytes = (size_t)batch * kMaxLevels * 8 * kCtrPad * sizeof(int);
-    const size_t dbytes = (size_t)kMaxLevels * batch * kCtrPad * sizeof(int);
-    const size_t cbytes = ((size_t)batch * npts * 8 + 127) / 128 * 128;
+    const size_t dbytes = ((size_t)kMaxLevels * batch + kLkFlagInts) * kCtrPad * sizeof(int);
+    const size_t lbytes = ((size_t)batch * npts * 8 + 127) / 128 * 128;   // one level's carried points
+    const size_t cbytes = lbytes * g.nlev;
     if ((rc = ensure(c, c->Abuf, abytes + 2 * (qbytes + dbytes + cbytes))) != MDX_OK) return rc;
     const int par = parity < 0 ? 0 : parity;
     uint8_t* base = c->Abuf.as<uint8_t>() + abytes + par * (qbytes + dbytes + cbytes);
-    a.carry = parity < 0 ? nullptr : reinterpret_cast<float*>(base + qbytes + dbytes);
+    a.carry = reinterpret_cast<float*>(base + qbytes + dbytes);
+    a.carry_lstride = (long long)(lbytes / sizeof(float));
     HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
                                   reinterpret_cast<int*>(base), prev_ready, c->iter2, c->flowev,
                                   reinterpret_cast<int*>(base + qbytes), c->prm.call_pipelining ? c->lvl_done : nullptr,
-                                  par, out_free));
+                                  par, out_free, c->iter2 ? c->redo_ev : nullptr));
     return MDX_OK;
 }
 

@@ -102,8 +102,10 @@ struct LkArgs {
     float min_eig;
     double eps2;
     float* next_pts;         // [batch][npts][2]
-    float* carry;            // LK v2: [batch][npts][2] the points carried between levels > 0 (level 0
-                             // reads it, writes next_pts); null: next_pts carries them
+    float* carry;            // LK v2: per level l > 0 a [batch][npts][2] array (at carry + l *
+                             // carry_lstride) of the points level l leaves for level l-1; level 0
+                             // writes next_pts.  null: next_pts carries them (levels in sequence only)
+    long long carry_lstride; // floats between two levels' carried-point arrays
     uint8_t* status;         // [batch][npts]
     ClassPlan plan;          // LK v2 only
     const int16_t* cmap;     // [level][axis][128] residue -> class index
@@ -117,8 +119,11 @@ struct LkArgs {
                              // the level launches run one after another
     int done_stride;
     int dep_groups;          // > 0: groups per pair of the coarser level, which a group waits for
-    int* err;                // dataflow: [0] group waits, [1] gate waits that timed out (read and
-                             // cleared at the context's sync points: mdx_sync returns MDX_EHIP)
+    int* err;                // dataflow statistics, read and cleared at the context's sync points:
+                             // [0] group waits and [1] gate waits that gave up, [2] levels recomputed
+    int* lflags;             // dataflow: the call's per-level flags (kLkFlag* below, zeroed with
+                             // `done`); null: no dataflow
+    int redo;                // 1: this launch is level `level`'s conditional recompute (kLkFlag*)
     int spin_max;            // dataflow wait bound in s_sleep(8) polls; < 0: fault injection (every
                              // wait counts as timed out at once; tests)
     int flow_cap;            // dataflow: percent of the resident waves one iteration launch takes
@@ -133,6 +138,17 @@ struct LkArgs {
 constexpr int kCtrPad = 32;
 // default dataflow wait bound: s_sleep(8) polls, ~0.1 s
 constexpr int kLkSpinDefault = 1 << 19;
+// Dataflow fallback flags of one call (LkArgs::lflags, ints kCtrPad apart, zeroed with the retire
+// counters): level l's give-ups (a group wait or the gate before it gave up: the level's results may
+// be wrong), whether level l was recomputed (so every finer level must be too), and the queue heads
+// of the recompute launches ([level][XCD]).
+constexpr int kLkFlagGiveup = 0;
+constexpr int kLkFlagRedone = kMaxLevels;
+constexpr int kLkFlagQueue = 2 * kMaxLevels;
+constexpr int kLkFlagInts = kLkFlagQueue + 8 * kMaxLevels;
+// persistent waves of a recompute launch: cheap when it exits at once (the common case), and a
+// recompute of the finest level at 1080p x 32 still takes only tens of ms
+constexpr int kLkRedoWaves = 512;
 
 // Core rows [lo, hi) of one pyramid level (row-band mode: what a band's LK reads)
 struct RowSpan {
@@ -193,7 +209,7 @@ hipError_t launch_traj_update(hipStream_t s, int npts, const float* next_pts, co
 // + 1 events (no timing) used to order the two streams.  prev_ready (may be null): recorded by the
 // caller once the first frames' pyramids exist; the aux work waits on it instead of on everything
 // enqueued on s so far (the second frames' pyramids may still be in flight on s).
-// Dataflow (s2 and flow_ev[2] non-null, done: kMaxLevels x batch ints): the level launches alternate
+// Dataflow (s2 and flow_ev[2] non-null, done: kMaxLevels x batch + kLkFlagInts counters): the level launches alternate
 // between s and s2, so level L-1 starts in level L's tail; its groups wait for their pair's level-L
 // groups (done counters).  Used when every XCD's work range holds two or more whole pairs (batch a
 // multiple of 8, at least 16) and pairs' next_pts do not share 128-B lines (npts % 16 == 0).
@@ -204,10 +220,15 @@ hipError_t launch_traj_update(hipStream_t s, int npts, const float* next_pts, co
 // the next call's first level can start on the other stream while this call's classify / fit / warp
 // run on s; qctr and done must then be the parity's own counters and a.carry non-null, and out_free
 // (the previous call's outputs read) is waited for before level 0 writes next_pts / status.
+// Dataflow fallback: a group whose wait gives up (the coarser level's launch was not dispatched in
+// time: a preempted, shared or serialized device) abandons its level, which then drains without
+// computing; right behind each level's launch, on its stream and after the coarser level's (redo_ev,
+// kMaxLevels events), a recompute launch re-runs the level in sequence if it gave up or the coarser
+// level was recomputed, and exits at once otherwise.  Results are then always exact.
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
                         float4* Ab, int* qctr, hipEvent_t prev_ready = nullptr, hipStream_t s2 = nullptr,
                         hipEvent_t* flow_ev = nullptr, int* done = nullptr, hipEvent_t* lvl_done = nullptr,
-                        int parity = 0, hipEvent_t out_free = nullptr);
+                        int parity = 0, hipEvent_t out_free = nullptr, hipEvent_t* redo_ev = nullptr);
 // Grid rows [gy0, gy1) only (a row band; others are neither written nor counted).  cand != null:
 // row-band mode -- the band's count and first four accepted points go to *cand (one record per
 // pair) instead of a fit.

@@ -745,6 +745,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
     const uint32_t off0 = (uint32_t)(cb - (long long)p0 * ngroups);   // cb's group within pair p0
     const int np = ce > cb ? (int)((ce - 1) / ngroups) - p0 + 1 : 1;
     int* ctr = qctr + (level * 8 + xcd) * kCtrPad;
+    if (a.redo) {
+        // the level's recompute: only if it gave up, or the coarser level was recomputed (its
+        // carried points changed after this level read them); levels then run in sequence
+        int need = __hip_atomic_load(a.lflags + (kLkFlagGiveup + level) * kCtrPad, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        if (level < a.maxl)
+            need |= __hip_atomic_load(a.lflags + (kLkFlagRedone + level + 1) * kCtrPad, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+        if (!need) return;
+        if (blockIdx.x == 0 && lane == 0) {
+            __hip_atomic_store(a.lflags + (kLkFlagRedone + level) * kCtrPad, 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(a.err + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ctr = a.lflags + (kLkFlagQueue + level * 8 + xcd) * kCtrPad;
+    }
+    // this level's give-up flag (dataflow): set by the first wait that gives up or by the gate
+    int* const giveup = a.lflags ? a.lflags + (kLkFlagGiveup + level) * kCtrPad : nullptr;
     const ClassLevel& C = a.plan.lv[level];
     const Level L = a.g.lv[level];
     // buffer addressing: descriptors over the range's class slabs and next-frame pyramids (the
@@ -778,7 +796,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
             if (a.dbg)
                 a.dbg[((long long)pair * a.g.nlev + level) * a.npts + pt] = make_float4(npx, npy, (float)iters, (float)status);
             const float2 v = make_float2(npx, npy);
-            float* dst = (a.carry && level > 0) ? a.carry : a.next_pts;
+            float* dst = (a.carry && level > 0) ? a.carry + level * a.carry_lstride : a.next_pts;
             if (a.done)   // read by the next level's launch while this one runs: write-through (sc1)
                 __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst) + po,
                                    __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -828,28 +846,40 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                         npy = (float)(q.gy * a.pixel_step) * scale;
                     } else {
                         float2 p = make_float2(0.f, 0.f);
+                        const float* src = a.carry ? a.carry + (level + 1) * a.carry_lstride : a.next_pts;
                         if (a.dep_groups) {
                             // dataflow: the coarser level may still run -- wait until every group of
                             // this pair has retired there (bounded: its waves are resident and
-                            // drain their queue), then read the carried points past L1
+                            // drain their queue), then read the carried points past L1.  A wait
+                            // that gives up abandons the level (every later wait sees the flag):
+                            // its groups drain without computing, and its recompute launch
+                            // (launch_lk_v2) runs it again once the coarser level is done.
                             if (sl == 0 && !gave_up) {
                                 // polls back off (1 .. 16 sleeps between loads): thousands of
                                 // waiting waves polling one line would load its L2 channel
                                 const int* d = a.done + ((level + 1) * a.done_stride + pair) * kCtrPad;
                                 int slept = 0, gap = 1;
-                                if (a.spin_max < 0) gave_up = true;   // fault injection (tests)
-                                while (!gave_up &&
+                                bool mine = false;
+                                if (a.spin_max < 0) mine = true;   // fault injection (tests)
+                                while (!mine &&
                                        __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.dep_groups) {
                                     if (slept >= a.spin_max) {
-                                        gave_up = true;
+                                        mine = true;
+                                        break;
+                                    }
+                                    if (__hip_atomic_load(giveup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0) {
+                                        gave_up = true;   // another wait (or the gate) gave up
                                         break;
                                     }
                                     for (int i = 0; i < gap; i++) __builtin_amdgcn_s_sleep(8);
                                     slept += gap;
                                     gap = gap < 16 ? 2 * gap : 16;
                                 }
-                                if (gave_up)   // this slot's results may be wrong: say so
+                                if (mine) {
+                                    gave_up = true;
+                                    __hip_atomic_fetch_add(giveup, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                     __hip_atomic_fetch_add(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                }
                             }
                             // The hand-off is MI355X_MICROARCH.md's measured form (table row 1):
                             // every carried point stored sc1, each storing wave's vmcnt(0) before
@@ -858,15 +888,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                             // (wavefront scope: no instruction) keeps the loads below the poll.
                             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                             if (q.valid)
-                                p = __builtin_bit_cast(float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(a.carry ? a.carry : a.next_pts) + po,
+                                p = __builtin_bit_cast(float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(src) + po,
                                                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                         } else if (q.valid) {
-                            p = reinterpret_cast<const float2*>(a.carry ? a.carry : a.next_pts)[po];
+                            p = reinterpret_cast<const float2*>(src)[po];
                         }
                         npx = p.x * 2.f;
                         npy = p.y * 2.f;
                     }
                     act = Dinv > 0.f;   // real point, window inside, eigenvalue / determinant tests passed
+                    // an abandoned level retires its groups at once (its recompute redoes them)
+                    if (a.dep_groups && __shfl((int)gave_up, slot * LPS)) act = false;
                     status = (level == 0 && q.valid && !act) ? 0 : 1;
                     nx = npx - HALFW;
                     ny = npy - HALFW;
@@ -1081,28 +1113,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
 // next level, launched beside the coarser level's whole queue, took half the chip and spun (both
 // launches ~2x slower); gated on the queues alone, one pair per XCD (4K x 8) left every next-level
 // wave polling its pair's counter (LK 3x slower).  Bounded like the group waits, and counted the
-// same way when the bound is hit (err[1]).
+// same way when the bound is hit (err[1]); the gated level is then abandoned at once (giveup: its
+// flag), since its waits could only time out too, and its recompute launch runs it.
 __global__ __launch_bounds__(64) void k_lk_gate(const int* __restrict__ qctr, long long T, const int* __restrict__ done,
                                                 int dep_groups, int ngroups_next, long long T_next, int* __restrict__ err,
-                                                int spin_max)
+                                                int spin_max, int* __restrict__ giveup)
 {
     const int x = threadIdx.x;
-    if (x >= 8) return;
-    const long long cb = T * x / 8, ce = T * (x + 1) / 8;
-    const long long cbn = T_next * x / 8;
-    const int pf = cbn < T_next ? (int)(cbn / ngroups_next) : -1;
-    bool ready = false;
-    for (int t = 0; t < spin_max; t++) {
-        const bool dry = __hip_atomic_load(qctr + x * kCtrPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ce - cb;
-        const bool first =
-            pf < 0 || __hip_atomic_load(done + pf * kCtrPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= dep_groups;
-        if (dry && first) {
-            ready = true;
-            break;
+    bool ready = true;   // lanes 0..7: XCD x's ranges
+    if (x < 8) {
+        const long long cb = T * x / 8, ce = T * (x + 1) / 8;
+        const long long cbn = T_next * x / 8;
+        const int pf = cbn < T_next ? (int)(cbn / ngroups_next) : -1;
+        ready = false;
+        for (int t = 0; t < spin_max; t++) {
+            const bool dry = __hip_atomic_load(qctr + x * kCtrPad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ce - cb;
+            const bool first = pf < 0 || __hip_atomic_load(done + pf * kCtrPad, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT) >= dep_groups;
+            if (dry && first) {
+                ready = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
         }
-        __builtin_amdgcn_s_sleep(8);
     }
-    if (!ready) __hip_atomic_fetch_add(err + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!__all(ready) && x == 0) {   // one count per gate
+        __hip_atomic_fetch_add(err + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(giveup, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // persistent waves for k_lk_iter: what the current device keeps resident at once (cached per
@@ -1166,13 +1204,14 @@ static void launch_iter(hipStream_t s, int batch, const LkArgs& a, const uint8_t
     const int need = (int)std::min<long long>(((long long)batch * ngroups + S - 1) / S, 1 << 30);
     int res = lk_iter_resident<G, UW>();
     if (a.done) res = res * std::min(std::max(a.flow_cap, 10), 100) / 100;   // the context's (MDX_LK_CAP)
-    const int W = std::max(8, std::min((need + 7) / 8, res / 8) * 8);
+    int W = std::max(8, std::min((need + 7) / 8, res / 8) * 8);
+    if (a.redo) W = std::max(8, std::min(W, kLkRedoWaves));
     hipLaunchKernelGGL((k_lk_iter<G, UW>), dim3(W), dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups, batch);
 }
 
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
                         float4* Ab, int* qctr, hipEvent_t prev_ready, hipStream_t s2, hipEvent_t* flow_ev, int* done,
-                        hipEvent_t* lvl_done, int parity, hipEvent_t out_free)
+                        hipEvent_t* lvl_done, int parity, hipEvent_t out_free, hipEvent_t* redo_ev)
 {
     // An XCD range spans at most ceil(n/8) + 1 pairs; its class slabs (and pyramids) must stay
     // addressable by 32-bit buffer offsets, so very large batches of large frames run in
@@ -1194,7 +1233,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         b.pyr2 = a.pyr2 + (long long)p * a.g.img_bytes;
         b.der = a.der + (long long)p * a.g.der_words;
         b.next_pts = a.next_pts + (long long)p * a.npts * 2;
-        b.carry = a.carry ? a.carry + (long long)p * a.npts * 2 : nullptr;
+        b.carry = a.carry ? a.carry + (long long)p * a.npts * 2 : nullptr;   // carry_lstride: whole batch
         b.status = a.status + (long long)p * a.npts;
         if (p) b.dbg = nullptr;   // the trace covers the first sub-batch
         uint8_t* bcls = cls + (long long)p * a.plan.bytes_per_pair;
@@ -1250,15 +1289,17 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         // no two pairs' carried points may share a 128-B line; with one pair per XCD (batch 8) the
         // next level can only start once the whole level is done there, and the dataflow measured
         // 1.5% slower than levels in sequence, so it needs at least two
-        const bool flow = aux && s2 && flow_ev && done && a.err && nb % 8 == 0 && nb >= 16 && a.npts % 16 == 0 &&
-                          (reinterpret_cast<uintptr_t>(b.next_pts) & 127) == 0 &&
-                          (reinterpret_cast<uintptr_t>(b.carry) & 127) == 0;
+        const bool flow = aux && s2 && flow_ev && done && redo_ev && a.err && b.carry && nb % 8 == 0 && nb >= 16 &&
+                          a.npts % 16 == 0 && (reinterpret_cast<uintptr_t>(b.next_pts) & 127) == 0 &&
+                          (reinterpret_cast<uintptr_t>(b.carry) & 127) == 0 && (a.carry_lstride % 32) == 0;
+        int* lflags = flow ? done + (long long)kMaxLevels * nb * kCtrPad : nullptr;
         // the even levels' stream (the first level's) and the odd levels'; parity 1 swaps them so
         // that this call's first level does not queue behind the previous call's fit / warp on s
         const bool swap = flow && parity && b.carry;
         hipStream_t s0 = swap ? s2 : s, s1 = swap ? s : s2;
         if (flow) {
-            if (hipError_t e = hipMemsetAsync(done, 0, sizeof(int) * kMaxLevels * nb * kCtrPad, s0)) return e;
+            if (hipError_t e = hipMemsetAsync(done, 0, sizeof(int) * ((long long)kMaxLevels * nb + kLkFlagInts) * kCtrPad, s0))
+                return e;
             if (hipError_t e = hipEventRecord(flow_ev[0], s0)) return e;   // counters zeroed, front end done
             if (hipError_t e = hipStreamWaitEvent(s1, flow_ev[0], 0)) return e;
         }
@@ -1278,6 +1319,8 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             bl.done = flow ? done : nullptr;
             bl.done_stride = nb;
             bl.dep_groups = 0;
+            bl.lflags = lflags;
+            bl.redo = 0;
             if (flow && l < a.maxl) {
                 const ClassLevel& Cp = a.plan.lv[l + 1];
                 bl.dep_groups = (Cp.nxp / Cp.G) * a.nyg;
@@ -1286,7 +1329,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
                 const int ng = (C.nxp / C.G) * a.nyg;
                 hipLaunchKernelGGL(k_lk_gate, dim3(1), dim3(64), 0, st, bq + (l + 1) * 8 * kCtrPad,
                                    (long long)nb * bl.dep_groups, done + (l + 1) * nb * kCtrPad, bl.dep_groups, ng,
-                                   (long long)nb * ng, a.err, a.spin_max);
+                                   (long long)nb * ng, a.err, a.spin_max, lflags + (kLkFlagGiveup + l) * kCtrPad);
             }
             const float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             switch (C.G * 1000 + C.UW) {
@@ -1294,6 +1337,26 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
                 LK_SHAPES
 #undef LK_CASE
             default: return hipErrorInvalidValue;
+            }
+            if (flow) {
+                // the level's recompute, behind it on its stream and behind the coarser level's
+                // (launch and recompute): exits at once unless the level gave up or the coarser
+                // one was recomputed.  The planes / A sums it reads are released (lvl_done) after it.
+                if (l < a.maxl) {
+                    if (hipError_t e = hipStreamWaitEvent(st, redo_ev[l + 1], 0)) return e;
+                    LkArgs br = bl;
+                    br.done = nullptr;
+                    br.dep_groups = 0;
+                    br.redo = 1;
+                    br.dbg = nullptr;
+                    switch (C.G * 1000 + C.UW) {
+#define LK_CASE(g, uw) case g * 1000 + uw: launch_iter<g, uw>(st, nb, br, bcls, bA, bq, l); break;
+                        LK_SHAPES
+#undef LK_CASE
+                    default: return hipErrorInvalidValue;
+                    }
+                }
+                if (hipError_t e = hipEventRecord(redo_ev[l], st)) return e;
             }
             if (lvl_done) {
                 if (hipError_t e = hipEventRecord(lvl_done[l], st)) return e;

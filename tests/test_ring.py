@@ -102,3 +102,18 @@ def test_ring_pushes_in_flight(mdx, ctx, oracle):
         ctx.ring_push(buf, 5)
         _compare(ctx.ring_trajectory(w, h, 5),
                  oracle.flow_trajectory(frames[k - 4:k + 1], pixel_step=10, nthreads=8), f"pinned push {k}")
+
+
+@pytest.mark.gpu
+def test_pinned_views_keep_the_block_alive(mdx):
+    """A plain-ndarray view of a page-locked array (np.asarray, .view(np.ndarray),
+    np.ascontiguousarray as ring_push takes it) keeps the block alive after the PinnedArray itself
+    is gone: numpy collapses a view's base chain to the lowest buffer object, which owns the block."""
+    import gc
+    a = mdx.host_empty((64, 64))
+    views = [np.asarray(a), a.view(np.ndarray), np.ascontiguousarray(a)]
+    del a
+    gc.collect()
+    for i, v in enumerate(views):
+        v[...] = i + 1                                    # use after free if the block was released
+        assert int(v.sum()) == (i + 1) * 64 * 64
