@@ -714,6 +714,24 @@ def main():
         cs = rctx.stage_ms()
         copy_ms = cs["warp_diff"] / max(cs["calls"], 1)
         copy_gbs = alg_bytes / (copy_ms * 1e-3) / 1e9
+        # the same launch with a projective H (every non-degenerate first-4 fit is projective): the
+        # tests' perspective matrix (tests/test_warp_gpu.py "projective"), per-pixel W and 32 / W
+        Hp = np.array([[1.002, 0.013, -2.5], [-0.011, 0.995, 1.75], [2.1e-5, -1.3e-5, 1.0]])
+        rctx.h2d(eH, np.ascontiguousarray(np.broadcast_to(Hp, (RB, 3, 3)), dtype=np.float64))
+        for _ in range(2):
+            rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
+        rctx.device_sync()
+        rctx.enable_timing(True)
+        for _ in range(args.steps):
+            rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
+        rctx.device_sync()
+        ps_ = rctx.stage_ms()
+        proj_ms = ps_["warp_diff"] / max(ps_["calls"], 1)
+        proj_gbs = alg_bytes / (proj_ms * 1e-3) / 1e9
+        projective = dict(avg_launch_us=round(proj_ms * 1e3, 2), achieved=round(proj_gbs, 1),
+                          frac=round(proj_gbs / HBM_PEAK_GBS, 4), launch_over_affine=round(proj_ms / launch_ms, 3),
+                          H=Hp.ravel().tolist(),
+                          workload=f"{rw}x{rh} gray, {RB} pairs per launch, projective H (M6, M7 != 0)")
         pmc = stamped_pmc(args.pmc_json, "config", f"{rw}x{rh}x{RB}")
         traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
         kt = stamped_pmc(os.path.join(ROOT, "profiles", "warp_kernel_trace.json"), "config", f"{rw}x{rh}x{RB}")
@@ -727,7 +745,8 @@ def main():
                     frac_of_copy_ceiling=round(achieved / copy_gbs, 4),
                     kernel_trace=({k: kt[k] for k in ("launch", "k_warp_diff", "k_warp_prep", "k_stream3",
                                                        "frac_of_copy_ceiling", "source") if k in kt}
-                                  if kt else None))
+                                  if kt else None),
+                    projective=projective)
         for p in (e1, e2, eH, eM):
             rctx.dev_free(p)
         rctx.close()

@@ -311,6 +311,9 @@ int mdx_stage_ms(mdx_ctx* ctx, int stage, float* ms);
 /* Test hook: copy an internal buffer of the last call to the host (0: per-(pair, level,
  * point) float4 LK gradient sums; 1: per-level LK trace when MDX_LK_DEBUG=1 at create). */
 int mdx_debug_copy(mdx_ctx* ctx, int which, void* dst, size_t bytes);
+/* Test hook: d_out[i] = 32 / d_in[i] through the projective warp's FP64 division (device buffers,
+ * queued on the context stream); equal to IEEE division for |d_in[i]| in [2^-100, 2^100]. */
+int mdx_debug_div32(mdx_ctx* ctx, const double* d_in, double* d_out, int n);
 
 /* Measurement probe, no reference counterpart: the memory ceiling of k_warp_diff's access mix.
  * d_mask[i] = |d_a[i] - d_b[i]| > thresh ? 255 : 0 over n bytes (n a multiple of 16, pointers

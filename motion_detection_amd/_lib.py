@@ -38,6 +38,7 @@ EXPORTED = [
     "mdx_srand", "mdx_rand", "mdx_fit_subspace", "mdx_device_pci", "mdx_build_info",
     "mdx_ring_push", "mdx_ring_trajectory", "mdx_ring_reset", "mdx_input_ready",
     "mdx_host_alloc", "mdx_host_free", "mdx_probe_stream3_dev", "mdx_lk_fallbacks",
+    "mdx_debug_div32",
 ]
 
 # csrc/Makefile STAMPED: the files whose bytes the library's provenance stamp hashes, in order
@@ -148,6 +149,9 @@ def lib() -> C.CDLL:
     L.mdx_flow_warp_diff_batch_dev.restype = C.c_int
     L.mdx_warp_diff_dev.argtypes = [vp, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int, C.c_size_t, vp, vp]
     L.mdx_warp_diff_dev.restype = C.c_int
+    if hasattr(L, "mdx_debug_div32"):
+        L.mdx_debug_div32.argtypes = [vp, vp, vp, C.c_int]
+        L.mdx_debug_div32.restype = C.c_int
     if hasattr(L, "mdx_lk_fallbacks"):
         L.mdx_lk_fallbacks.argtypes = [vp, C.POINTER(C.c_longlong)]
         L.mdx_lk_fallbacks.restype = C.c_int

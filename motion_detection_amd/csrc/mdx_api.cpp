@@ -1418,6 +1418,14 @@ extern "C" int mdx_debug_copy(mdx_ctx* c, int which, void* dst, size_t bytes)
     return MDX_OK;
 }
 
+extern "C" int mdx_debug_div32(mdx_ctx* c, const double* d_in, double* d_out, int n)
+{
+    if (!c || !d_in || !d_out || n <= 0) return MDX_EINVAL;
+    HIP_OR_RETURN(c, hipSetDevice(c->device));
+    HIP_OR_RETURN(c, launch_div32(c->stream, d_in, d_out, n));
+    return MDX_OK;
+}
+
 extern "C" void* mdx_host_alloc(size_t bytes)
 {
     void* p = nullptr;

@@ -255,6 +255,7 @@ hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long lo
                             const uint8_t* g2, long long g2_stride, int g2_pitch, int w, int h,
                             const PairFit* fits, uint8_t* mask, long long mask_stride, int thresh, void* scratch,
                             size_t scratch_bytes, int row0 = 0, int row1 = -1);
+hipError_t launch_div32(hipStream_t s, const double* in, double* out, int n);   // test hook
 hipError_t launch_stream3(hipStream_t s, size_t n, const uint8_t* a, const uint8_t* b, uint8_t* o, int thresh);
 hipError_t launch_export_fit(hipStream_t s, int batch, const PairFit* fits, double* H, int* num_vectors);
 

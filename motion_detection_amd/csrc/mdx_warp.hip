@@ -40,8 +40,13 @@
 //     out-of-range offset and rows past the band fall outside the mask descriptor, so the row
 //     loop is branch-free.  ~17 VALU per pixel (4 of them FP64), vs ~23 for the 64x128-tile
 //     design before it (rocprofv3 SQ_INSTS_VALU).
-// Everything else (perspective M, small frames, huge or far-away footprints) takes the general
-// per-pixel path, exact for any input.
+// Projective M (M6 or M7 != 0, e.g. every non-degenerate first-4 fit) takes the same tiles: the
+// tile's footprint is the bounding box of its reference blocks' corner images (the homography maps
+// the tile to a convex quadrilateral when W keeps one sign over it) widened by one pixel for the
+// rounding of interior pixels, and each pixel evaluates the reference's W = W0 + M6*x1, the
+// correctly rounded 32/W and its own rounded products (warp_rows<.., PROJ = true>).
+// Everything else (W changing sign over a tile, small frames, huge or far-away footprints) takes
+// the general per-pixel path, exact for any input.
 #include "mdx_internal.h"
 
 #include <limits.h>
@@ -98,7 +103,7 @@ __device__ __forceinline__ uint8_t warp_px_general(const double* M, const uint8_
 }
 
 struct TileInfo {
-    double wd;         // 32 / M8 (affine: W = M8 everywhere), 0 when M8 == 0
+    double wd;         // 32 / M8 (affine: W = M8 everywhere), 0 when M8 == 0; projective: unused
     int fast;          // 1: fast path usable for this tile
     int sxa, sya;      // staged origin (sxa multiple of 16)
     int sw, sh;        // staged width (bytes), height (rows)
@@ -107,10 +112,15 @@ struct TileInfo {
 // Bounds of the tile's taps, from the reference arithmetic at the corners of its (one or two)
 // reference blocks, one corner per lane of an aligned group of 8 (lane = its index in the group;
 // every lane of the group returns the result); fast = every |X|, |Y| < 2^30 (no clamp, magic
-// rounding exact) and the footprint fits the staging buffer.
+// rounding exact) and the footprint fits the staging buffer.  Affine M: X and Y are monotone in x
+// and y inside a block, so the corners bound every pixel's taps exactly.  Projective M: W is
+// linear in (x, y), so if it has one sign (and a sane magnitude) at the corners it has it over the
+// whole tile, the tile's image is the convex hull of the corner images, and X / W, Y / W take their
+// extremes at the corners (linear-fractional); interior pixels' rounded coordinates can exceed the
+// corners' by one 1/32 unit, so the footprint is widened by one pixel on every side.
 __device__ TileInfo tile_info(const double* M, int x0, int y0, int w, int yend, int lane)
 {
-    const double Wd = M[8] != 0.0 ? 32.0 / M[8] : 0.0;
+    const bool affine = M[6] == 0.0 && M[7] == 0.0;
     const int nb = (x0 + kBW < w) ? 2 : 1;                       // reference blocks in the tile
     const int b = ((lane >> 2) & 1) < nb ? ((lane >> 2) & 1) : 0;
     const int xb = x0 + kBW * b;
@@ -119,9 +129,20 @@ __device__ TileInfo tile_info(const double* M, int x0, int y0, int w, int yend, 
     const int x1 = (c & 1) ? cxl : 0, y = y0 + ((c & 2) ? cyl : 0);
     const double X0 = M[0] * xb + M[1] * y + M[2];
     const double Y0 = M[3] * xb + M[4] * y + M[5];
+    double Wd = M[8] != 0.0 ? 32.0 / M[8] : 0.0;
+    int wsign = 1;
+    if (!affine) {                                               // the reference's per-pixel W
+        const double W0 = M[6] * xb + M[7] * y + M[8];
+        const double Wv = W0 + M[6] * x1;
+        Wd = Wv != 0.0 ? 32.0 / Wv : 0.0;
+        const double aw = fabs(Wv);
+        // W in [2^-100, 2^100] at every corner (so over the tile): div32's range
+        wsign = (aw >= 0x1p-100 && aw <= 0x1p100) ? (Wv > 0.0 ? 1 : 2) : 0;
+    }
     const double px = (X0 + M[0] * x1) * Wd, py = (Y0 + M[3] * x1) * Wd;
     const double lim = 1073741824.0;   // 2^30
-    int ok = (px > -lim && px < lim && py > -lim && py < lim) ? 1 : 0;
+    int ok = (px > -lim && px < lim && py > -lim && py < lim && wsign != 0) ? 1 : 0;
+    int smin = wsign, smax = wsign;
     int sx = 0, sy = 0;
     if (ok) {
         sx = ((int)__builtin_rint(px)) >> 5;
@@ -135,6 +156,12 @@ __device__ TileInfo tile_info(const double* M, int x0, int y0, int w, int yend, 
         sy_lo = min(sy_lo, __shfl_xor(sy_lo, m, 8));
         sy_hi = max(sy_hi, __shfl_xor(sy_hi, m, 8));
         ok = min(ok, __shfl_xor(ok, m, 8));
+        smin = min(smin, __shfl_xor(smin, m, 8));
+        smax = max(smax, __shfl_xor(smax, m, 8));
+    }
+    if (!affine) {
+        ok = ok && smin == smax;                               // W keeps its sign over the tile
+        sx_lo -= 1; sy_lo -= 1; sx_hi += 1; sy_hi += 1;        // interior rounding margin
     }
     TileInfo t;
     t.wd = Wd;
@@ -173,24 +200,54 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, lon
 // without, 230-234 with nt on the footprint too, 222-224 with nt on the mask only; on a second box
 // 211-220 with nt against 223-229 without.
 constexpr int kCpStream = 2;   // buffer aux bit 1 = nt
-template <bool POW2, bool ROWCHK>
+typedef __attribute__((address_space(3))) const double lds_d1;
+// 32 / d correctly rounded, for |d| in [2^-100, 2^100] (tile_info keeps the fast path there): the
+// compiler's IEEE double division without its v_div_scale / v_div_fixup steps, which only act on
+// exponents far outside that range (huge quotients, denormals, inf / nan) -- two Newton steps on
+// v_rcp_f64, the quotient, and the final FMA correction that rounds it correctly.  8 FP64
+// instructions instead of 11.  tests/test_warp_gpu.py checks it bit for bit against IEEE division
+// over that range (mdx_debug_div32).
+__device__ __forceinline__ double div32(double d)
+{
+    const double r0 = __builtin_amdgcn_rcp(d);
+    const double e0 = __builtin_fma(-d, r0, 1.0);
+    const double r1 = __builtin_fma(r0, e0, r0);
+    const double e1 = __builtin_fma(-d, r1, 1.0);
+    const double r2 = __builtin_fma(r1, e1, r1);
+    const double q0 = 32.0 * r2;
+    const double rem = __builtin_fma(-d, q0, 32.0);
+    return __builtin_fma(rem, r2, q0);
+}
+// PROJ: projective M -- per pixel W = W0 + fl(M6*x1) (W0 per row and block from wp, tw[k] = fl(M6*x1)),
+// Wd = 32 / W correctly rounded (the reference's W ? 32/W : 0; nonzero on the fast path), and the
+// product (X0 + M0*x1) * Wd rounded before the magic add rounds it to an integer, as in the reference
+template <bool POW2, bool ROWCHK, bool PROJ = false>
 __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t src_base, int nvalid,
                                           __amdgpu_buffer_rsrc_t g2rs, uint32_t g2off, int g2s,
                                           __amdgpu_buffer_rsrc_t mrs, uint32_t moff, int ms, const double* tx,
-                                          const double* ty, double Wd, double mX, double mY, uint32_t bias)
+                                          const double* ty, double Wd, double mX, double mY, uint32_t bias,
+                                          lds_d1* wp = nullptr, const double* tw = nullptr)
 {
     uint32_t G[kTH / 8];
 #pragma unroll
     for (int i = 0; i < kTH / 8; i++) G[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * g2s, kCpStream);
 #pragma unroll
     for (int i = 0; i < kTH / 8; i++) {
-        const d2v xy = xyp[ROWCHK ? (i < nvalid ? 16 * i : 0) : 16 * i];   // rows are 2 blocks x 16 B apart
+        const int ri = ROWCHK ? (i < nvalid ? i : 0) : i;
+        const d2v xy = xyp[16 * ri];                      // rows are 2 blocks x 16 B apart
+        double w0 = 0.0;
+        if constexpr (PROJ) w0 = wp[16 * ri];             // rows are 2 blocks x 8 B apart
         uint32_t xs_[4], ys_[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const double ax = xy.x + tx[k], ay = xy.y + ty[k];
             double rx, ry;
-            if (POW2) {                                   // (X0 + M0*x1) * Wd exact: one rounding
+            if constexpr (PROJ) {
+                const double Wv = w0 + tw[k];
+                const double Wk = div32(Wv);              // = 32.0 / Wv (|Wv| in [2^-100, 2^100] on a fast tile)
+                rx = ax * Wk + mX;
+                ry = ay * Wk + mY;
+            } else if (POW2) {                            // (X0 + M0*x1) * Wd exact: one rounding
                 rx = __builtin_fma(ax, Wd, mX);
                 ry = __builtin_fma(ay, Wd, mY);
             } else {                                      // round the product, then to integer
@@ -399,7 +456,7 @@ __global__ __launch_bounds__(256) void k_warp_prep(const PairFit* __restrict__ f
 // on (x, y) only, so a band is exactly the full frame's rows.  The tile's footprint bounds and
 // the pair's fixed-point tables come from k_warp_prep, so the setup has one barrier: footprint
 // DMA, gray2 loads and the per-row-block table in flight together, then the row loop.
-__global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_warp_diff(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
                                                    const uint8_t* __restrict__ g2, long long g2_stride, int g2_pitch,
                                                    int w, int h, int bw0, const PairFit* __restrict__ fits,
                                                    uint8_t* __restrict__ mask, long long mask_stride, int thresh,
@@ -408,6 +465,7 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[64];             // weight table (FP64 rows)
     __shared__ __attribute__((aligned(16))) double s_xy[kTH][2][2];         // (X0, Y0) per row, block
+    __shared__ __attribute__((aligned(16))) double s_w0[kTH][2];            // projective: W0 per row, block
     __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
     __shared__ __attribute__((aligned(16))) uint4 s_fx[kTH][2];             // fixed point: (A_x, A_y, flag)
 
@@ -447,7 +505,7 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     const uint8_t* src = g1 + (long long)pair * g1_stride;
     const bool affine = (M[6] == 0.0) && (M[7] == 0.0);
     // fast path only over dword-aligned rows with reference blocks of 64 (uniform per workgroup)
-    const bool try_fast = affine && bw0 == kBW && vec_ok;
+    const bool try_fast = bw0 == kBW && vec_ok;
     const TileInfo t = tinfo[(long long)pair * (nbx * nby) + tile];   // uniform: scalar loads
     if (!try_fast || !t.fast) {
         // ---- general path: per pixel, global gathers
@@ -464,7 +522,7 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
     // ---- fast path
     const double Wd = t.wd;
     // 32/M8 a power of two -> (X0 + M0*x1) * Wd is exact: the fixed-point rows (warp_rows_fx)
-    const bool pow2 = Wd != 0.0 && (__double_as_longlong(Wd) & 0x000fffffffffffffLL) == 0;
+    const bool pow2 = affine && Wd != 0.0 && (__double_as_longlong(Wd) & 0x000fffffffffffffLL) == 0;
     if (!pow2 && tid < 32) {
         s_tab[2 * tid] = (uint32_t)(32 - tid) | ((uint32_t)tid << 16);
         s_tab[2 * tid + 1] = (uint32_t)(64 * (32 - tid)) | ((uint32_t)(64 * tid) << 16);
@@ -515,6 +573,7 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
         const double Y0 = M[3] * xb + M[4] * y + M[5];
         s_xy[r][b][0] = X0;
         s_xy[r][b][1] = Y0;
+        if (!affine) s_w0[r][b] = M[6] * xb + M[7] * y + M[8];
         if (pow2) {
             const double fx_scale = 524288.0;                        // 2^19
             const uint32_t Ax = floor_lo((Wd * X0 + 0.5 - 32.0 * t.sxa) * fx_scale);
@@ -555,7 +614,7 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
         else
             warp_rows_fx<true>(fxp, xyp, src_base, nvalid, G, mrs, moff, 8 * w, bx, by, M[0],
                                M[3], x1b, Wd, mX, mY, bias);
-    } else {
+    } else if (affine) {
         double tx[4], ty[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -565,6 +624,18 @@ __global__ __launch_bounds__(256) void k_warp_diff(const uint8_t* __restrict__ g
         }
         warp_rows<false, true>(xyp, tabp, src_base, nvalid, g2rs, g2off, 8 * g2_pitch, mrs, moff, 8 * w, tx, ty, Wd, mX,
                                mY, bias);
+    } else {
+        double tx[4], ty[4], tw[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            tx[k] = M[0] * (x1b + k);
+            ty[k] = M[3] * (x1b + k);
+            tw[k] = M[6] * (x1b + k);
+            asm volatile("" : "+v"(tx[k]), "+v"(ty[k]), "+v"(tw[k]));
+        }
+        lds_d1* wp = (lds_d1*)(&s_w0[r0][blk]);
+        warp_rows<false, true, true>(xyp, tabp, src_base, nvalid, g2rs, g2off, 8 * g2_pitch, mrs, moff, 8 * w, tx, ty,
+                                     0.0, mX, mY, bias, wp, tw);
     }
 }
 
@@ -595,6 +666,19 @@ hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long lo
                        (int)grid.x, (int)grid.y, tinfo, prep);
     hipLaunchKernelGGL(k_warp_diff, grid, dim3(256), 0, s, g1, g1_stride, g1_pitch, g2, g2_stride, g2_pitch, w, h, bw0,
                        fits, mask, mask_stride, thresh, vec_ok, row0, row1, tinfo, prep);
+    return hipGetLastError();
+}
+
+// Test hook (mdx_debug_div32): div32 over n values.
+__global__ void k_div32(const double* __restrict__ in, double* __restrict__ out, int n)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = div32(in[i]);
+}
+
+hipError_t launch_div32(hipStream_t s, const double* in, double* out, int n)
+{
+    hipLaunchKernelGGL(k_div32, dim3((n + 255) / 256), dim3(256), 0, s, in, out, n);
     return hipGetLastError();
 }
 

@@ -43,6 +43,13 @@ def _H(kind, w, h, Ht):
         "tie_rows": np.array([[1.0, 1.0 / 2048, 0.0], [0.0, 1.0, 0.0], [0.0, 0.0, 1.0]]),
         "near_tie": np.array([[1.0, 0.0, 0.5 / 32 + 2.0 ** -28], [0.0, 1.0, -0.5 / 32 - 2.0 ** -29], [0.0, 0.0, 1.0]]),
         "near_tie_rot": _rot(0.25, 1.0, 0.5 / 32 + 2.0 ** -27, 0.5 / 32 - 2.0 ** -26, w / 2, h / 2),
+        # projective fast path (per-pixel W and 32 / W): perspective in x and y; a tiny perspective term
+        # on a 1/64-px translation, so X sits within ~x^2 2^-35 px of a rounding tie (the division's
+        # last bits decide); and a horizon (W = 0) inside the frame, where tiles fall back
+        "proj_xy": np.array([[0.98, 0.021, 4.5], [-0.017, 1.01, -3.25], [-3.1e-5, 2.4e-5, 1.0]]),
+        "proj_near_tie": np.linalg.inv(np.array([[1.0, 0.0, 1.0 / 64], [0.0, 1.0, -1.0 / 64],
+                                                 [2.0 ** -40, 2.0 ** -41, 1.0]])),
+        "proj_horizon": np.linalg.inv(np.array([[1.0, 0.0, 0.0], [0.0, 1.0, 0.0], [-1.0 / (0.6 * w), 0.0, 1.0]])),
     }[kind]
 
 
@@ -76,7 +83,8 @@ def _run(mdx, ctx, oracle, g1, g2, Hs, thresh):
 
 
 KINDS = ["true", "identity", "tie_translation", "tie_scale_half", "rot5", "flip_x", "zoom_in", "zoom_out",
-         "far_away", "m8_not_pow2", "projective", "singular", "tie_rows", "near_tie", "near_tie_rot"]
+         "far_away", "m8_not_pow2", "projective", "singular", "tie_rows", "near_tie", "near_tie_rot", "proj_xy",
+         "proj_near_tie", "proj_horizon"]
 
 
 @pytest.mark.parametrize("w,h", [(640, 480), (1000, 300), (1984, 70), (128, 64), (132, 65), (68, 33)])
@@ -103,6 +111,48 @@ def test_warp_4k_true_h(mdx, wctx, oracle):
     w, h = 3840, 2160
     a, b, Ht = mdx.synth_pair(20141105, w, h, 1)
     _run(mdx, wctx, oracle, a[None], b[None], [Ht], 190)
+
+
+def test_warp_4k_projective(mdx, wctx, oracle):
+    """The bench's projective roofline sub-line geometry (roofline.projective): 4K with the tests'
+    perspective H, and its near-tie variant, both on the projective fast path."""
+    w, h = 3840, 2160
+    a, b, Ht = mdx.synth_pair(20141105, w, h, 1)
+    a2, b2, _ = mdx.synth_pair(20141106, w, h, 1)
+    _run(mdx, wctx, oracle, np.stack([a, a2]), np.stack([b, b2]),
+         [_H("projective", w, h, Ht), _H("proj_near_tie", w, h, Ht)], 190)
+
+
+def test_div32_is_ieee_division(mdx, wctx):
+    """The projective fast path's 32 / W (mdx_warp.hip div32: the IEEE division sequence without its
+    range-scaling steps) equals correctly rounded IEEE division bit for bit over its range
+    |W| in [2^-100, 2^100]: random mantissas over every exponent, both signs, and hard mantissas
+    (all ones, powers of two, near one)."""
+    import ctypes as C
+    rng = np.random.default_rng(11)
+    n = 1 << 20
+    e = rng.integers(-100, 100, n)
+    m = 1.0 + rng.random(n)
+    d = np.ldexp(m, e) * np.where(rng.random(n) < 0.5, -1.0, 1.0)
+    hard = []
+    for ex in range(-100, 100):
+        for mm in (1.0, np.nextafter(2.0, 0.0), np.nextafter(1.0, 2.0), 1.5, 1.0 + 2.0 ** -26, 2.0 - 2.0 ** -26):
+            hard += [np.ldexp(mm, ex), -np.ldexp(mm, ex)]
+    d[:len(hard)] = hard
+    d = np.ascontiguousarray(d[(np.abs(d) >= 2.0 ** -100) & (np.abs(d) <= 2.0 ** 100)])
+    di, do = wctx.dev_alloc(d.nbytes), wctx.dev_alloc(d.nbytes)
+    try:
+        wctx.h2d(di, d)
+        assert mdx.lib().mdx_debug_div32(wctx._h, C.c_void_p(di), C.c_void_p(do), len(d)) == 0
+        wctx.sync()
+        out = np.empty_like(d)
+        wctx.d2h(out, do)
+    finally:
+        wctx.dev_free(di)
+        wctx.dev_free(do)
+    ref = 32.0 / d
+    bad = np.nonzero(out.view(np.uint64) != ref.view(np.uint64))[0]
+    assert bad.size == 0, f"{bad.size} of {len(d)} differ, first W {d[bad[:4]].tolist()}"
 
 
 def test_copy_ceiling_probe(mdx, wctx):
