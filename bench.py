@@ -546,6 +546,7 @@ def main():
     ap.add_argument("--inflight", type=int, default=2, help="c4: frames in flight per GPU (one context each)")
     ap.add_argument("--no-live", action="store_true", help="skip the node's live trajectory + RANSAC leg")
     ap.add_argument("--no-4k", action="store_true", help="skip the whole-path 4K leg (config C2)")
+    ap.add_argument("--no-ransac", action="store_true", help="skip the MDX_FIT_RANSAC whole-path leg")
     ap.add_argument("--rehearse", action="store_true",
                     help="allow more ranks than visible GPUs (they share device 0; n_gpus counts distinct devices)")
     ap.add_argument("--no-lk-roofline", action="store_true", help="skip the LK iteration census (profiling runs)")
@@ -679,6 +680,61 @@ def main():
             kctx.dev_free(p)
         kctx.close()
         del k1, k2
+
+    # ---- MDX_FIT_RANSAC (not in the reference; parity with it N/A): the headline step with the
+    # deterministic RANSAC fit instead of first-4, so the warp runs on a real, projective fit
+    ransac = None
+    if not args.no_ransac and not args.only_roofline and args.config == "1080p":
+        rkw = dict(pixel_step=ps, min_vector_size=1.0, call_pipelining=pipe, fit_mode=mdx.FIT_RANSAC)
+        qg1, qg2, _, quniq = make_batch(w, h, B, unique, SEED0 + 1000 * D.rank, threads)
+        qctx = open_ctx(D, w, h, B, **rkw)
+        q1, q2 = qctx.dev_alloc(qg1.nbytes), qctx.dev_alloc(qg2.nbytes)
+        qo = {k: qctx.dev_alloc(sz) for k, sz in dict(np=B * n * 8, st=B * n, vec=B * n * 32, mask=B * w * h,
+                                                      H=B * 72, num=B * 4).items()}
+        qctx.h2d(q1, qg1); qctx.h2d(q2, qg2)
+
+        def stepq():
+            qctx.flow_warp_diff_batch_dev(B, q1, q2, w, h, w, w * h, mdx.FMT_GRAY8, d_next_pts=qo["np"],
+                                          d_status=qo["st"], d_vectors=qo["vec"], d_mask=qo["mask"], d_H=qo["H"],
+                                          d_num_vectors=qo["num"])
+        for _ in range(max(1, args.warmup)):
+            stepq()
+        qctx.device_sync()
+        qctx.enable_timing(True)
+        D.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            stepq()
+        qctx.device_sync()
+        D.barrier()
+        rateq, elq = throughput(D, float(args.steps * B * w * h), time.perf_counter() - t0)
+        qs = qctx.stage_ms()
+        qst = {k: round(v / max(qs["calls"], 1), 4) for k, v in qs.items() if k in ("classify_fit", "warp_diff")}
+        qH = np.empty((B, 9))
+        qctx.d2h(qH, qo["H"])
+        qpar = None
+        if not args.no_parity:
+            from oracle import pyoracle   # untimed checker (test infrastructure)
+            qpar = {"checked_pairs": 0, "mismatched_pairs": 0}
+            qm = np.empty((B, h, w), np.uint8)
+            qctx.d2h(qm, qo["mask"])
+            for i, (a, b_, _) in enumerate(quniq):
+                r = pyoracle.calculate_optical_flow(a, b_, nthreads=host_cores()["available"], pixel_step=ps,
+                                                    min_vector_size=1.0, fit_mode=2, simd=True)
+                ok = (np.array_equal(qH[i].view(np.uint64), r["H"].ravel().view(np.uint64)) and
+                      np.array_equal(qm[i], r["mask"]))
+                qpar["checked_pairs"] += 1
+                qpar["mismatched_pairs"] += 0 if ok else 1
+        ransac = dict(workload=f"{w}x{h} gray x {B}, the headline step with fit_mode MDX_FIT_RANSAC "
+                               f"({mdx.default_params().ransac_iters} hypotheses, 3 px): NOT in the reference, "
+                               f"parity with the reference N/A (oracle-pinned, bit-exact)",
+                      value=round(rateq / 1e6, 2), unit="Mpixels/s", ms_per_step=round(elq / args.steps * 1e3, 3),
+                      stage_ms_per_step=qst, H_pair0=qH[0].tolist(),
+                      warp_projective=bool(qH[0][6] != 0.0 or qH[0][7] != 0.0), parity_vs_oracle=qpar)
+        for p in [q1, q2] + list(qo.values()):
+            qctx.dev_free(p)
+        qctx.close()
+        del qg1, qg2
 
     # ---- north-star kernel: fused warp+diff at 4K with the generator's true H
     roof = None
@@ -824,6 +880,7 @@ def main():
         "num_vectors_pair0": int(num[0]),
         "lk_fallbacks": fallbacks,
         "full_path_4k": full4k,
+        "full_path_ransac": ransac,
         "live_path": live,
     }
     if D.rank == 0:

@@ -45,6 +45,13 @@ extern "C" {
 #define MDX_FIT_FIRST4   0   /* reference: getPerspectiveTransform on the first 4 accepted
                                 vectors in x-major grid order (:120) */
 #define MDX_FIT_EXTERNAL 1   /* caller supplies H (forward, frame1 -> frame2) per pair */
+#define MDX_FIT_RANSAC   2   /* NOT in the reference (parity with it N/A): deterministic RANSAC over
+                                all accepted vectors -- mdx_params.ransac_iters hypotheses, each the
+                                reference's own 4-point getPerspectiveTransform on 4 accepted vectors
+                                drawn by a counter-based generator (splitmix64 of ransac_seed,
+                                hypothesis, draw); the hypothesis with the most inliers (reprojection
+                                error <= ransac_thresh px; first on ties) is H, without a refit.
+                                Restated in oracle/ and bit-exact there. */
 
 /* mdx_fit_subspace arithmetic (see its comment below). */
 #define MDX_SUBSPACE_F64 0   /* double Householder basis and residuals (stable; the default) */
@@ -63,6 +70,10 @@ typedef struct {
     int    fit_mode;         /* MDX_FIT_FIRST4 (default) or MDX_FIT_EXTERNAL */
     int    subspace_precision; /* mdx_fit_subspace arithmetic: MDX_SUBSPACE_F64 (default) or _F32 */
     int    call_pipelining;  /* 0 (default) or 1: consecutive device-entry calls overlap (below) */
+    int    ransac_iters;     /* MDX_FIT_RANSAC hypotheses, 1..1024 (default 128) */
+    double ransac_thresh;    /* MDX_FIT_RANSAC inlier reprojection error, px (default 3.0, as
+                                OpenCV findHomography's ransacReprojThreshold) */
+    uint32_t ransac_seed;    /* MDX_FIT_RANSAC generator seed (default 20141105) */
 } mdx_params;
 
 /*

@@ -24,7 +24,7 @@ MDX_ENOMEM = -3
 MDX_EDEGENERATE = 1
 
 FMT_GRAY8, FMT_RGB8, FMT_BGR8 = 0, 1, 2
-FIT_FIRST4, FIT_EXTERNAL = 0, 1
+FIT_FIRST4, FIT_EXTERNAL, FIT_RANSAC = 0, 1, 2
 SUBSPACE_F64, SUBSPACE_F32 = 0, 1
 
 # every symbol include/mdx.h declares (checked by tests/test_abi.py)
@@ -65,7 +65,8 @@ class MdxParams(C.Structure):
     _fields_ = [("win", C.c_int), ("max_level", C.c_int), ("max_iters", C.c_int), ("eps", C.c_double),
                 ("min_eig", C.c_float), ("thresh", C.c_int), ("pixel_step", C.c_int),
                 ("min_vector_size", C.c_double), ("fit_mode", C.c_int), ("subspace_precision", C.c_int),
-                ("call_pipelining", C.c_int)]
+                ("call_pipelining", C.c_int), ("ransac_iters", C.c_int), ("ransac_thresh", C.c_double),
+                ("ransac_seed", C.c_uint32)]
 
 
 class MdxError(RuntimeError):

@@ -76,6 +76,7 @@ struct mdx_ctx {
     DevBuf straj, sdata, sq, scnt, scols, sres, sout, sbest;      // subspace RANSAC
     DevBuf ring_pyr, ring_der, rin;          // resident frame ring (mdx_ring_*)
     DevBuf wscr;                             // k_warp_prep's per-pair / per-tile tables
+    DevBuf rsc;                              // MDX_FIT_RANSAC scratch (list, hypotheses, counts)
     std::vector<int> ring_order;             // held slots, oldest first
     int ring_cap = 0, ring_w = 0, ring_h = 0, ring_ml = -1;
     bool lk_debug = false;
@@ -129,6 +130,9 @@ extern "C" void mdx_default_params(mdx_params* p)
     p->fit_mode = MDX_FIT_FIRST4;
     p->subspace_precision = MDX_SUBSPACE_F64;
     p->call_pipelining = 0;
+    p->ransac_iters = 128;
+    p->ransac_thresh = 3.0;
+    p->ransac_seed = 20141105u;
 }
 
 extern "C" int mdx_grid_count(int w, int h, int ps)
@@ -142,7 +146,12 @@ static int check_params(const mdx_params* p, std::string* why)
     if (p->win != kWin) { *why = "only win == 40 (the reference constant) is supported"; return 0; }
     if (p->max_level < 0 || p->max_level >= kMaxLevels) { *why = "max_level out of range [0, 7]"; return 0; }
     if (p->pixel_step <= 0) { *why = "pixel_step must be > 0 (reference leaves it unset: UB)"; return 0; }
-    if (p->fit_mode != MDX_FIT_FIRST4 && p->fit_mode != MDX_FIT_EXTERNAL) { *why = "bad fit_mode"; return 0; }
+    if (p->fit_mode != MDX_FIT_FIRST4 && p->fit_mode != MDX_FIT_EXTERNAL && p->fit_mode != MDX_FIT_RANSAC) {
+        *why = "bad fit_mode";
+        return 0;
+    }
+    if (p->ransac_iters < 1 || p->ransac_iters > kRansacMaxIters) { *why = "ransac_iters must be in [1, 1024]"; return 0; }
+    if (!(p->ransac_thresh >= 0.0) || !(p->ransac_thresh < 1e6)) { *why = "ransac_thresh must be in [0, 1e6)"; return 0; }
     if (p->subspace_precision != MDX_SUBSPACE_F64 && p->subspace_precision != MDX_SUBSPACE_F32) {
         *why = "bad subspace_precision";
         return 0;
@@ -460,7 +469,7 @@ extern "C" int mdx_destroy(mdx_ctx* c)
                       &c->cls, &c->Abuf, &c->ctab, &c->dbg, &c->csum, &c->tin, &c->tcur, &c->tnp, &c->tst,
                       &c->ttraj, &c->tlen, &c->tvec, &c->tstart, &c->tnum, &c->tflag, &c->straj, &c->sdata, &c->sq,
                       &c->scnt, &c->scols, &c->sres, &c->sout, &c->sbest, &c->ring_pyr, &c->ring_der, &c->rin,
-                      &c->errw, &c->wscr};
+                      &c->errw, &c->wscr, &c->rsc};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (c->err_host) (void)hipHostFree(c->err_host);
@@ -850,8 +859,19 @@ static int run_pipeline(mdx_ctx* c, int batch, const uint8_t* d_img1, const uint
     }
     mark(c, 4);
     if ((rc = ensure(c, c->csum, classify_scratch_bytes(batch, npts))) != MDX_OK) return rc;
+    RansacArgs ra{};
+    if (P.fit_mode == MDX_FIT_RANSAC && !cand) {
+        if ((rc = ensure(c, c->rsc, ransac_scratch_bytes(batch, npts, P.ransac_iters))) != MDX_OK) return rc;
+        uint8_t* base = c->rsc.as<uint8_t>();
+        ra.iters = P.ransac_iters;
+        ra.thresh = P.ransac_thresh;
+        ra.seed = P.ransac_seed;
+        ra.list = reinterpret_cast<int*>(base);
+        ra.hyps = reinterpret_cast<double*>(base + (((size_t)batch * npts * 4 + 7) & ~(size_t)7));
+        ra.counts = reinterpret_cast<int*>(reinterpret_cast<uint8_t*>(ra.hyps) + (size_t)batch * P.ransac_iters * 72);
+    }
     HIP_OR_RETURN(c, launch_classify_fit(s, batch, d_np, d_st, npts, ny, gy0, gy1, P.pixel_step, P.min_vector_size, d_vec,
-                                         fits, P.fit_mode, d_Hext, c->csum.p, cand));
+                                         fits, P.fit_mode, d_Hext, c->csum.p, cand, &ra));
     mark(c, 5);
     if (cand) {
         // mdx_band_fit_warp_dev reads the latest band call's pyramids (same frame pair), whichever
@@ -944,7 +964,7 @@ extern "C" int mdx_flow_warp_diff(mdx_ctx* c, const uint8_t* img1, const uint8_t
     HIP_OR_RETURN(c, hipMemcpyAsync(&num, c->num.p, 4, hipMemcpyDeviceToHost, s));
     HIP_OR_RETURN(c, hipStreamSynchronize(s));
     if (num_vectors) *num_vectors = num;
-    if (c->prm.fit_mode == MDX_FIT_FIRST4 && num < 4) return MDX_EDEGENERATE;
+    if (c->prm.fit_mode != MDX_FIT_EXTERNAL && num < 4) return MDX_EDEGENERATE;
     return MDX_OK;
 }
 

@@ -229,13 +229,27 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
                         float4* Ab, int* qctr, hipEvent_t prev_ready = nullptr, hipStream_t s2 = nullptr,
                         hipEvent_t* flow_ev = nullptr, int* done = nullptr, hipEvent_t* lvl_done = nullptr,
                         int parity = 0, hipEvent_t out_free = nullptr, hipEvent_t* redo_ev = nullptr);
+// MDX_FIT_RANSAC (mdx_kernels.hip k_ransac_*): device scratch and parameters
+constexpr int kRansacMaxIters = 1024;
+struct RansacArgs {
+    int iters;
+    double thresh;
+    uint32_t seed;
+    int* list;       // [batch][npts] accepted grid indices, x-major
+    double* hyps;    // [batch][iters][9]
+    int* counts;     // [batch][iters]
+};
+inline size_t ransac_scratch_bytes(int batch, int npts, int iters)
+{
+    return (size_t)batch * npts * 4 + (size_t)batch * iters * 72 + (size_t)batch * iters * 4 + 256;
+}
 // Grid rows [gy0, gy1) only (a row band; others are neither written nor counted).  cand != null:
 // row-band mode -- the band's count and first four accepted points go to *cand (one record per
 // pair) instead of a fit.
 hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
                                int ny, int gy0, int gy1, int pixel_step, double min_vector_size, double* vectors,
                                PairFit* fits, int fit_mode, const double* H_external, void* scratch,
-                               mdx_band_cand* cand);
+                               mdx_band_cand* cand, const RansacArgs* ransac = nullptr);
 // Merge nrec band records (first four accepted overall = four smallest indices) and fit
 hipError_t launch_band_fit(hipStream_t s, int nrec, const mdx_band_cand* cands, PairFit* fit, int w, int h, int y0,
                            int y1);

@@ -961,47 +961,49 @@ __device__ double dev_hypot(double x, double y)
 // lapack.cpp JacobiSVDImpl_<double> (one-sided Jacobi on A's columns, eps 10*DBL_EPSILON,
 // max(m,30) sweeps, descending sort) then SVBkSb (threshold 2*DBL_EPSILON*sum(w)).
 // The working arrays live in LDS (one lane runs the solve): as private arrays they were
-// scratch memory, whose latency every dependent step of the sweep paid.
+// scratch memory, whose latency every dependent step of the sweep paid.  Element e of the
+// working set is fw[e * S]: S = 1 for one lane (k_fit), S = lanes for a lane-interleaved set
+// (k_ransac_hyp: lane l's element e at fw[e * S + l], conflict-free across lanes).
 struct FitWork {
     double At[64], Vt[64], W[8], bv[8], x[8];
 };
-__device__ __forceinline__ void dev_perspective_fit(const float* src, const float* dst, double* M, FitWork& fw)
+constexpr int kFitWorkDoubles = 152;
+template <int S>
+__device__ __forceinline__ void dev_perspective_fit_s(const float* src, const float* dst, double* M, double* fw)
 {
-    double* At = fw.At;
-    double* Vt = fw.Vt;
-    double* W = fw.W;
-    double* bv = fw.bv;
-    double* x = fw.x;
-    for (int i = 0; i < 64; i++) At[i] = 0.0;
+#define AT(e) fw[(e) * S]
+#define VT(e) fw[(64 + (e)) * S]
+#define WV(e) fw[(128 + (e)) * S]
+#define BV(e) fw[(136 + (e)) * S]
+#define XV(e) fw[(144 + (e)) * S]
+    for (int i = 0; i < 64; i++) AT(i) = 0.0;
     for (int i = 0; i < 4; i++) {
         const float sx = src[2 * i], sy = src[2 * i + 1], dx = dst[2 * i], dy = dst[2 * i + 1];
         // A[i][c] stored as At[c*8 + i]; rows i (x equations) and i+4 (y equations)
-        At[0 * 8 + i] = sx; At[1 * 8 + i] = sy; At[2 * 8 + i] = 1.0;
-        At[3 * 8 + i + 4] = sx; At[4 * 8 + i + 4] = sy; At[5 * 8 + i + 4] = 1.0;
-        At[6 * 8 + i] = (double)(-sx * dx);
-        At[7 * 8 + i] = (double)(-sy * dx);
-        At[6 * 8 + i + 4] = (double)(-sx * dy);
-        At[7 * 8 + i + 4] = (double)(-sy * dy);
-        bv[i] = dx;
-        bv[i + 4] = dy;
+        AT(0 * 8 + i) = sx; AT(1 * 8 + i) = sy; AT(2 * 8 + i) = 1.0;
+        AT(3 * 8 + i + 4) = sx; AT(4 * 8 + i + 4) = sy; AT(5 * 8 + i + 4) = 1.0;
+        AT(6 * 8 + i) = (double)(-sx * dx);
+        AT(7 * 8 + i) = (double)(-sy * dx);
+        AT(6 * 8 + i + 4) = (double)(-sx * dy);
+        AT(7 * 8 + i + 4) = (double)(-sy * dy);
+        BV(i) = dx;
+        BV(i + 4) = dy;
     }
     const int m = 8, n = 8;
     const double eps = DBL_EPSILON * 10;
     for (int i = 0; i < n; i++) {
         double sd = 0;
-        for (int k = 0; k < m; k++) { const double t = At[i * m + k]; sd += t * t; }
-        W[i] = sd;
-        for (int k = 0; k < n; k++) Vt[i * n + k] = 0;
-        Vt[i * n + i] = 1;
+        for (int k = 0; k < m; k++) { const double t = AT(i * m + k); sd += t * t; }
+        WV(i) = sd;
+        for (int k = 0; k < n; k++) VT(i * n + k) = 0;
+        VT(i * n + i) = 1;
     }
     for (int iter = 0; iter < 30; iter++) {
         bool changed = false;
         for (int i = 0; i < n - 1; i++)
             for (int j = i + 1; j < n; j++) {
-                double* Ai = At + i * m;
-                double* Aj = At + j * m;
-                double aa = W[i], p = 0, bb = W[j];
-                for (int k = 0; k < m; k++) p += Ai[k] * Aj[k];
+                double aa = WV(i), p = 0, bb = WV(j);
+                for (int k = 0; k < m; k++) p += AT(i * m + k) * AT(j * m + k);
                 if (fabs(p) <= eps * __builtin_sqrt(aa * bb)) continue;
                 p *= 2;
                 const double beta = aa - bb, gamma = dev_hypot(p, beta);
@@ -1016,58 +1018,68 @@ __device__ __forceinline__ void dev_perspective_fit(const float* src, const floa
                 }
                 aa = bb = 0;
                 for (int k = 0; k < m; k++) {
-                    const double t0 = c * Ai[k] + s * Aj[k];
-                    const double t1 = -s * Ai[k] + c * Aj[k];
-                    Ai[k] = t0; Aj[k] = t1;
+                    const double ai = AT(i * m + k), aj = AT(j * m + k);
+                    const double t0 = c * ai + s * aj;
+                    const double t1 = -s * ai + c * aj;
+                    AT(i * m + k) = t0; AT(j * m + k) = t1;
                     aa += t0 * t0; bb += t1 * t1;
                 }
-                W[i] = aa; W[j] = bb;
+                WV(i) = aa; WV(j) = bb;
                 changed = true;
-                double* Vi = Vt + i * n;
-                double* Vj = Vt + j * n;
                 for (int k = 0; k < n; k++) {
-                    const double t0 = c * Vi[k] + s * Vj[k];
-                    const double t1 = -s * Vi[k] + c * Vj[k];
-                    Vi[k] = t0; Vj[k] = t1;
+                    const double vi = VT(i * n + k), vj = VT(j * n + k);
+                    const double t0 = c * vi + s * vj;
+                    const double t1 = -s * vi + c * vj;
+                    VT(i * n + k) = t0; VT(j * n + k) = t1;
                 }
             }
         if (!changed) break;
     }
     for (int i = 0; i < n; i++) {
         double sd = 0;
-        for (int k = 0; k < m; k++) { const double t = At[i * m + k]; sd += t * t; }
-        W[i] = __builtin_sqrt(sd);
+        for (int k = 0; k < m; k++) { const double t = AT(i * m + k); sd += t * t; }
+        WV(i) = __builtin_sqrt(sd);
     }
     for (int i = 0; i < n - 1; i++) {
         int j = i;
-        for (int k = i + 1; k < n; k++) if (W[j] < W[k]) j = k;
+        for (int k = i + 1; k < n; k++) if (WV(j) < WV(k)) j = k;
         if (i != j) {
-            double t = W[i]; W[i] = W[j]; W[j] = t;
-            for (int k = 0; k < m; k++) { t = At[i * m + k]; At[i * m + k] = At[j * m + k]; At[j * m + k] = t; }
-            for (int k = 0; k < n; k++) { t = Vt[i * n + k]; Vt[i * n + k] = Vt[j * n + k]; Vt[j * n + k] = t; }
+            double t = WV(i); WV(i) = WV(j); WV(j) = t;
+            for (int k = 0; k < m; k++) { t = AT(i * m + k); AT(i * m + k) = AT(j * m + k); AT(j * m + k) = t; }
+            for (int k = 0; k < n; k++) { t = VT(i * n + k); VT(i * n + k) = VT(j * n + k); VT(j * n + k) = t; }
         }
     }
     // Left singular vectors: rows with W[i] <= DBL_MIN are skipped by the back-substitution
     // threshold below, so only the normalisation of the others matters.
     for (int i = 0; i < n; i++) {
-        if (W[i] <= DBL_MIN) continue;
-        const double s = 1 / W[i];
-        for (int k = 0; k < m; k++) At[i * m + k] *= s;
+        if (WV(i) <= DBL_MIN) continue;
+        const double s = 1 / WV(i);
+        for (int k = 0; k < m; k++) AT(i * m + k) *= s;
     }
     double threshold = 0;
-    for (int i = 0; i < n; i++) { x[i] = 0; threshold += W[i]; }
+    for (int i = 0; i < n; i++) { XV(i) = 0; threshold += WV(i); }
     threshold *= DBL_EPSILON * 2;
     for (int i = 0; i < n; i++) {
-        double wi = W[i];
+        double wi = WV(i);
         if (fabs(wi) <= threshold) continue;
         wi = 1 / wi;
         double s = 0;
-        for (int j = 0; j < m; j++) s += At[i * m + j] * bv[j];
+        for (int j = 0; j < m; j++) s += AT(i * m + j) * BV(j);
         s *= wi;
-        for (int j = 0; j < n; j++) x[j] = x[j] + s * Vt[i * n + j];
+        for (int j = 0; j < n; j++) XV(j) = XV(j) + s * VT(i * n + j);
     }
-    for (int i = 0; i < 8; i++) M[i] = x[i];
+    for (int i = 0; i < 8; i++) M[i] = XV(i);
     M[8] = 1.;
+#undef AT
+#undef VT
+#undef WV
+#undef BV
+#undef XV
+}
+__device__ __forceinline__ void dev_perspective_fit(const float* src, const float* dst, double* M, FitWork& fw)
+{
+    static_assert(sizeof(FitWork) == kFitWorkDoubles * sizeof(double), "FitWork layout");
+    dev_perspective_fit_s<1>(src, dst, M, reinterpret_cast<double*>(&fw));
 }
 
 // lapack.cpp invert(DECOMP_LU) for 3x3 CV_64F: cofactors times 1/det3; det == 0 -> zeros.
@@ -1146,11 +1158,11 @@ __global__ __launch_bounds__(256) void k_classify(const float* __restrict__ next
 }
 
 __global__ __launch_bounds__(64) void k_fit(const float* __restrict__ next_pts, int npts, int ny, int pixel_step,
-                                            const BlockSummary* __restrict__ summ, int nblk, PairFit* __restrict__ fits,
+                                            BlockSummary* __restrict__ summ, int nblk, PairFit* __restrict__ fits,
                                             int fit_mode, const double* __restrict__ H_ext)
 {
     const int pair = blockIdx.x, lane = threadIdx.x;
-    const BlockSummary* S = summ + (long long)pair * nblk;
+    BlockSummary* S = summ + (long long)pair * nblk;
     int carry = 0;          // accepted points in blocks before the current chunk
     int pick[4] = {-1, -1, -1, -1};
     for (int b0 = 0; b0 < nblk; b0 += 64) {
@@ -1163,6 +1175,7 @@ __global__ __launch_bounds__(64) void k_fit(const float* __restrict__ next_pts, 
             if (lane >= d) incl += t;
         }
         const int excl = carry + incl - cnt;
+        if (fit_mode == MDX_FIT_RANSAC && b < nblk) S[b].pad_[0] = excl;   // k_ransac_compact's block offsets
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             // the block holding overall rank r (one lane at most), then broadcast its index
@@ -1182,10 +1195,12 @@ __global__ __launch_bounds__(64) void k_fit(const float* __restrict__ next_pts, 
     PairFit& f = fits[pair];
     const int total = carry;
     f.num_vectors = total;
-    if (fit_mode == 1) {
+    if (fit_mode == MDX_FIT_EXTERNAL) {
         for (int k = 0; k < 9; k++) f.H[k] = H_ext[(long long)pair * 9 + k];
         dev_invert3x3(f.H, f.Hinv);
         f.fit_status = 0;
+    } else if (fit_mode == MDX_FIT_RANSAC && total >= 4) {
+        f.fit_status = 0;                        // H / Hinv: k_ransac_pick
     } else if (total >= 4) {
         float src[8], dst[8];
         for (int r = 0; r < 4; r++) {
@@ -1203,6 +1218,158 @@ __global__ __launch_bounds__(64) void k_fit(const float* __restrict__ next_pts, 
         for (int k = 0; k < 9; k++) { f.H[k] = 0.0; f.Hinv[k] = 0.0; }
         f.fit_status = total == 0 ? 1 : 2;
     }
+}
+
+// ------------------------------------------------------------------ MDX_FIT_RANSAC (not in the reference)
+// Deterministic RANSAC over every accepted vector (include/mdx.h MDX_FIT_RANSAC, DESIGN.md §7d;
+// restated by oracle/mdx_oracle.c ora_fit_ransac, which the GPU equals bit for bit):
+//   k_ransac_compact  the accepted vectors' grid indices in x-major order (the reference's
+//                     src / dst order, optical_flow_calculator.cpp:78-117), from k_fit's block offsets
+//   k_ransac_hyp      one lane per hypothesis: 4 distinct draws from splitmix64(seed, h, draw, retry)
+//                     and the reference's getPerspectiveTransform on them (dev_perspective_fit_s,
+//                     the lane's working set interleaved in LDS)
+//   k_ransac_score    every accepted vector against every hypothesis: inlier iff
+//                     |H src - dst * w|^2 <= t^2 w^2 in FP64 (w the projective denominator), counts
+//                     added per workgroup
+//   k_ransac_pick     the hypothesis with the most inliers (lowest index on ties), its inverse
+__device__ __forceinline__ uint64_t ransac_mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// the reference's acceptance test of grid point i (k_classify's)
+__device__ __forceinline__ bool ransac_accepted(const float* next_pts, const uint8_t* status, long long o, int i, int ny,
+                                                int pixel_step, double mvs, float& sx, float& sy, float2& e)
+{
+    sx = (float)((i / ny) * pixel_step);
+    sy = (float)((i % ny) * pixel_step);
+    e = reinterpret_cast<const float2*>(next_pts)[o];
+    if (!status[o]) return false;
+    const float xd = e.x - sx, yd = e.y - sy;
+    return fabs((double)fabsf(xd)) > mvs || fabs((double)fabsf(yd)) > mvs;
+}
+
+__global__ __launch_bounds__(256) void k_ransac_compact(const float* __restrict__ next_pts,
+                                                        const uint8_t* __restrict__ status, int npts, int ny,
+                                                        int pixel_step, double mvs,
+                                                        const BlockSummary* __restrict__ summ, int* __restrict__ list)
+{
+    const int pair = blockIdx.y, blk = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    __shared__ int s_wcnt[4];
+    const int i = blk * 256 + tid;
+    bool acc = false;
+    if (i < npts) {
+        float sx, sy;
+        float2 e;
+        acc = ransac_accepted(next_pts, status, (long long)pair * npts + i, i, ny, pixel_step, mvs, sx, sy, e);
+    }
+    const unsigned long long bal = __ballot(acc);
+    if (lane == 0) s_wcnt[wave] = __popcll(bal);
+    __syncthreads();
+    int before = 0;
+    for (int w2 = 0; w2 < wave; w2++) before += s_wcnt[w2];
+    const int rank = before + __popcll(bal & ((1ull << lane) - 1ull));
+    const int off = summ[(long long)pair * gridDim.x + blk].pad_[0];
+    if (acc) list[(long long)pair * npts + off + rank] = i;
+}
+
+constexpr int kRansacLanes = 32;   // hypotheses per workgroup (LDS: 32 interleaved fit working sets)
+__global__ __launch_bounds__(64) void k_ransac_hyp(const float* __restrict__ next_pts, int npts, int ny, int pixel_step,
+                                                   const int* __restrict__ list, const PairFit* __restrict__ fits,
+                                                   int iters, uint32_t seed, double* __restrict__ hyps,
+                                                   int* __restrict__ counts)
+{
+    __shared__ double s_fw[kFitWorkDoubles * kRansacLanes];
+    const int pair = blockIdx.y, lane = threadIdx.x, h = blockIdx.x * kRansacLanes + lane;
+    if (lane >= kRansacLanes || h >= iters) return;
+    counts[(long long)pair * iters + h] = 0;
+    const int n = fits[pair].num_vectors;
+    if (fits[pair].fit_status != 0 || n < 4) return;
+    int idx[4];
+    for (int j = 0; j < 4; j++) {
+        for (uint32_t c = 0;; c++) {
+            const uint64_t x = ((uint64_t)seed << 32) | ((uint64_t)h << 20) | ((uint64_t)j << 16) | (uint64_t)(c & 0xffffu);
+            const int v = (int)(ransac_mix64(x) % (uint64_t)n);
+            bool dup = false;
+            for (int q = 0; q < j; q++) dup = dup || idx[q] == v;
+            if (!dup || c >= 0xffffu) {
+                idx[j] = v;
+                break;
+            }
+        }
+    }
+    float src[8], dst[8];
+    for (int j = 0; j < 4; j++) {
+        const int i = list[(long long)pair * npts + idx[j]];
+        src[2 * j] = (float)((i / ny) * pixel_step);
+        src[2 * j + 1] = (float)((i % ny) * pixel_step);
+        const float2 e = reinterpret_cast<const float2*>(next_pts)[(long long)pair * npts + i];
+        dst[2 * j] = e.x;
+        dst[2 * j + 1] = e.y;
+    }
+    double Hh[9];
+    dev_perspective_fit_s<kRansacLanes>(src, dst, Hh, s_fw + lane);
+    for (int k = 0; k < 9; k++) hyps[((long long)pair * iters + h) * 9 + k] = Hh[k];
+}
+
+__global__ __launch_bounds__(256) void k_ransac_score(const float* __restrict__ next_pts,
+                                                     const uint8_t* __restrict__ status, int npts, int ny,
+                                                     int pixel_step, double mvs, const double* __restrict__ hyps,
+                                                     int iters, double t2, const PairFit* __restrict__ fits,
+                                                     int* __restrict__ counts)
+{
+    __shared__ int s_cnt[kRansacMaxIters];
+    const int pair = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+    if (fits[pair].fit_status != 0 || fits[pair].num_vectors < 4) return;   // uniform per workgroup
+    for (int h = tid; h < iters; h += 256) s_cnt[h] = 0;
+    __syncthreads();
+    const int i = blockIdx.x * 256 + tid;
+    bool acc = false;
+    double sx = 0.0, sy = 0.0, dx = 0.0, dy = 0.0;
+    if (i < npts) {
+        float fsx, fsy;
+        float2 e;
+        acc = ransac_accepted(next_pts, status, (long long)pair * npts + i, i, ny, pixel_step, mvs, fsx, fsy, e);
+        sx = fsx; sy = fsy; dx = e.x; dy = e.y;
+    }
+    const double* Hp = hyps + (long long)pair * iters * 9;
+    for (int h = 0; h < iters; h++) {
+        const double* H = Hp + 9 * h;                 // uniform: scalar loads
+        const double nx = H[0] * sx + H[1] * sy + H[2];
+        const double nyv = H[3] * sx + H[4] * sy + H[5];
+        const double dd = H[6] * sx + H[7] * sy + H[8];
+        const double ex = nx - dx * dd, ey = nyv - dy * dd;
+        const bool in = acc && ex * ex + ey * ey <= t2 * (dd * dd);
+        const unsigned long long bal = __ballot(in);
+        if (lane == 0 && bal) atomicAdd(&s_cnt[h], __popcll(bal));
+    }
+    __syncthreads();
+    for (int h = tid; h < iters; h += 256)
+        if (s_cnt[h]) atomicAdd(&counts[(long long)pair * iters + h], s_cnt[h]);
+}
+
+__global__ __launch_bounds__(64) void k_ransac_pick(const double* __restrict__ hyps, const int* __restrict__ counts,
+                                                    int iters, PairFit* __restrict__ fits)
+{
+    const int pair = blockIdx.x, lane = threadIdx.x;
+    PairFit& f = fits[pair];
+    if (f.fit_status != 0 || f.num_vectors < 4) return;
+    int bc = -1, bh = 0;
+    for (int h = lane; h < iters; h += 64) {
+        const int cnt = counts[(long long)pair * iters + h];
+        if (cnt > bc) { bc = cnt; bh = h; }            // first max of this lane's (increasing) h
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const int oc = __shfl_xor(bc, m), oh = __shfl_xor(bh, m);
+        if (oc > bc || (oc == bc && oh < bh)) { bc = oc; bh = oh; }
+    }
+    if (lane != 0) return;
+    for (int k = 0; k < 9; k++) f.H[k] = hyps[((long long)pair * iters + bh) * 9 + k];
+    dev_invert3x3(f.H, f.Hinv);
 }
 
 // Row-band mode: the same block scan as k_fit, but the band's count and first four accepted
@@ -1605,7 +1772,8 @@ hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a)
 
 hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, const uint8_t* status, int npts,
                                int ny, int gy0, int gy1, int pixel_step, double mvs, double* vectors, PairFit* fits,
-                               int fit_mode, const double* H_external, void* scratch, mdx_band_cand* cand)
+                               int fit_mode, const double* H_external, void* scratch, mdx_band_cand* cand,
+                               const RansacArgs* ransac)
 {
     const int nblk = (npts + 255) / 256;
     BlockSummary* summ = reinterpret_cast<BlockSummary*>(scratch);
@@ -1617,6 +1785,17 @@ hipError_t launch_classify_fit(hipStream_t s, int batch, const float* next_pts, 
     else
         hipLaunchKernelGGL(k_fit, dim3(batch), dim3(64), 0, s, next_pts, npts, ny, pixel_step, summ, nblk, fits,
                            fit_mode, H_external);
+    if (fit_mode == MDX_FIT_RANSAC && !cand) {
+        if (!ransac || nblk == 0 || ransac->iters < 1 || ransac->iters > kRansacMaxIters) return hipErrorInvalidValue;
+        const RansacArgs& r = *ransac;
+        hipLaunchKernelGGL(k_ransac_compact, dim3(nblk, batch), dim3(256), 0, s, next_pts, status, npts, ny, pixel_step,
+                           mvs, summ, r.list);
+        hipLaunchKernelGGL(k_ransac_hyp, dim3((r.iters + kRansacLanes - 1) / kRansacLanes, batch), dim3(64), 0, s,
+                           next_pts, npts, ny, pixel_step, r.list, fits, r.iters, r.seed, r.hyps, r.counts);
+        hipLaunchKernelGGL(k_ransac_score, dim3(nblk, batch), dim3(256), 0, s, next_pts, status, npts, ny, pixel_step,
+                           mvs, r.hyps, r.iters, r.thresh * r.thresh, fits, r.counts);
+        hipLaunchKernelGGL(k_ransac_pick, dim3(batch), dim3(64), 0, s, r.hyps, r.counts, r.iters, fits);
+    }
     return hipGetLastError();
 }
 

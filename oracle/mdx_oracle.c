@@ -29,6 +29,10 @@ void ora_default_params(ora_params* p)
     p->thresh = 190;
     p->pixel_step = 10;
     p->min_vector_size = 1.0;
+    p->fit_mode = ORA_FIT_FIRST4;
+    p->ransac_iters = 128;
+    p->ransac_thresh = 3.0;
+    p->ransac_seed = 20141105u;
 }
 
 /* OpenCV borderInterpolate(p, len, BORDER_REFLECT_101) (core/src/copy.cpp). */
@@ -824,6 +828,66 @@ void ora_grid_points(int w, int h, int ps, float* pts)
         }
 }
 
+/* ---------------------------------------------------------------- RANSAC option -------- */
+/* The product's MDX_FIT_RANSAC (not in the reference): see mdx_oracle.h. */
+static uint64_t ransac_mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+int ora_fit_ransac(const float* src, const float* dst, int n, int iters, double thresh, uint32_t seed, double H[9],
+                   int* best_h)
+{
+    if (n < 4 || iters < 1) return -1;
+    const double t2 = thresh * thresh;
+    int bc = -1, bh = 0;
+    double Hb[9] = {0};
+    for (int h = 0; h < iters; h++) {
+        int idx[4];
+        for (int j = 0; j < 4; j++) {
+            for (uint32_t c = 0;; c++) {
+                const uint64_t x = ((uint64_t)seed << 32) | ((uint64_t)h << 20) | ((uint64_t)j << 16) | (uint64_t)(c & 0xffffu);
+                const int v = (int)(ransac_mix64(x) % (uint64_t)n);
+                int dup = 0;
+                for (int q = 0; q < j; q++) dup = dup || idx[q] == v;
+                if (!dup || c >= 0xffffu) {
+                    idx[j] = v;
+                    break;
+                }
+            }
+        }
+        float s4[8], d4[8];
+        for (int j = 0; j < 4; j++) {
+            s4[2 * j] = src[2 * idx[j]];
+            s4[2 * j + 1] = src[2 * idx[j] + 1];
+            d4[2 * j] = dst[2 * idx[j]];
+            d4[2 * j + 1] = dst[2 * idx[j] + 1];
+        }
+        double Hh[9];
+        ora_get_perspective_transform(s4, d4, Hh);
+        int cnt = 0;
+        for (int k = 0; k < n; k++) {
+            const double sx = src[2 * k], sy = src[2 * k + 1], dx = dst[2 * k], dy = dst[2 * k + 1];
+            const double nx = Hh[0] * sx + Hh[1] * sy + Hh[2];
+            const double ny = Hh[3] * sx + Hh[4] * sy + Hh[5];
+            const double dd = Hh[6] * sx + Hh[7] * sy + Hh[8];
+            const double ex = nx - dx * dd, ey = ny - dy * dd;
+            if (ex * ex + ey * ey <= t2 * (dd * dd)) cnt++;
+        }
+        if (cnt > bc) {
+            bc = cnt;
+            bh = h;
+            memcpy(Hb, Hh, sizeof(Hb));
+        }
+    }
+    memcpy(H, Hb, sizeof(Hb));
+    if (best_h) *best_h = bh;
+    return bc;
+}
+
 /* ---------------------------------------------------------------- whole path ---------- */
 int ora_calculate_optical_flow(const uint8_t* img1, const uint8_t* img2, int w, int h, int stride,
                                int fmt, const ora_params* prm, int nthreads,
@@ -848,6 +912,9 @@ int ora_calculate_optical_flow(const uint8_t* img1, const uint8_t* img2, int w, 
 
     int num = 0;
     float src4[8], dst4[8];
+    const int ransac = prm->fit_mode == ORA_FIT_RANSAC;
+    float* srcs = ransac ? (float*)malloc(sizeof(float) * 2 * (size_t)(npts > 0 ? npts : 1)) : NULL;
+    float* dsts = ransac ? (float*)malloc(sizeof(float) * 2 * (size_t)(npts > 0 ? npts : 1)) : NULL;
     for (int i = 0; i < npts; i++) {
         float sx = pts1[2 * i], sy = pts1[2 * i + 1];
         float ex = pts2[2 * i], ey = pts2[2 * i + 1];
@@ -860,6 +927,10 @@ int ora_calculate_optical_flow(const uint8_t* img1, const uint8_t* img2, int w, 
                     src4[2 * num] = sx; src4[2 * num + 1] = sy;
                     dst4[2 * num] = ex; dst4[2 * num + 1] = ey;
                 }
+                if (ransac) {
+                    srcs[2 * num] = sx; srcs[2 * num + 1] = sy;
+                    dsts[2 * num] = ex; dsts[2 * num + 1] = ey;
+                }
                 num++;
             } else if (v) { v[0] = sx; v[1] = sy; v[2] = 0.0; v[3] = 0.0; }
         } else if (v) { v[0] = -1.0; v[1] = -1.0; v[2] = 0.0; v[3] = 0.0; }
@@ -871,7 +942,10 @@ int ora_calculate_optical_flow(const uint8_t* img1, const uint8_t* img2, int w, 
     int fs;
     if (num >= 4) {
         fs = 0;
-        ora_get_perspective_transform(src4, dst4, Hm);
+        if (ransac)
+            ora_fit_ransac(srcs, dsts, num, prm->ransac_iters, prm->ransac_thresh, prm->ransac_seed, Hm, NULL);
+        else
+            ora_get_perspective_transform(src4, dst4, Hm);
         ora_invert3x3(Hm, Hi);
         if (mask) {
             uint8_t* warped = (uint8_t*)malloc((size_t)w * h);
@@ -889,7 +963,7 @@ int ora_calculate_optical_flow(const uint8_t* img1, const uint8_t* img2, int w, 
 
     ora_free_pyramid(&P1);
     ora_free_pyramid(&P2);
-    free(g1); free(g2); free(pts1); free(pts2); free(st);
+    free(g1); free(g2); free(pts1); free(pts2); free(st); free(srcs); free(dsts);
     return num;
 }
 

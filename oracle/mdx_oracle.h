@@ -44,7 +44,14 @@ typedef struct {
     int thresh;          /* threshold 190 (:127) */
     int pixel_step;      /* ROS param pixel_step (motion_detection_node.cpp:29) */
     double min_vector_size; /* ROS param min_vector_size, default 1.0 (node.cpp:44) */
+    /* NOT in the reference: the product's MDX_FIT_RANSAC option (include/mdx.h), restated below */
+    int fit_mode;            /* ORA_FIT_FIRST4 (default, the reference) or ORA_FIT_RANSAC */
+    int ransac_iters;        /* default 128 */
+    double ransac_thresh;    /* default 3.0 px */
+    uint32_t ransac_seed;    /* default 20141105 */
 } ora_params;
+#define ORA_FIT_FIRST4 0
+#define ORA_FIT_RANSAC 2
 
 void ora_default_params(ora_params* p);
 
@@ -87,6 +94,17 @@ int  ora_invert3x3(const double M[9], double Minv[9]);
 void ora_warp_perspective(const uint8_t* src, int w, int h, int sstride, const double M[9],
                           uint8_t* dst, int dstride, int nthreads);
 void ora_absdiff_threshold(const uint8_t* a, const uint8_t* b, int n, int thresh, uint8_t* mask);
+
+/* Deterministic RANSAC homography (the product's MDX_FIT_RANSAC; no reference counterpart, so
+ * parity with the reference is N/A -- this pins the GPU kernels k_ransac_*): over the n accepted
+ * vectors (src, dst) in x-major order, `iters` hypotheses; hypothesis h draws 4 distinct indices
+ * idx_j = splitmix64(seed << 32 | h << 20 | j << 16 | retry) % n and fits them with
+ * ora_get_perspective_transform (the reference's 4-point solver); a vector is an inlier of H iff
+ * ex^2 + ey^2 <= t^2 w^2 with w = H6 sx + H7 sy + H8, ex = (H0 sx + H1 sy + H2) - dx w, ey likewise
+ * (FP64, this evaluation order, t = thresh); the first hypothesis with the most inliers is H.
+ * Returns its inlier count (-1 when n < 4: H untouched); *best_h = its index if non-NULL. */
+int ora_fit_ransac(const float* src, const float* dst, int n, int iters, double thresh, uint32_t seed, double H[9],
+                   int* best_h);
 
 /* Grid of the reference (optical_flow_calculator.cpp:56-64): x-major order. */
 int  ora_grid_count(int w, int h, int pixel_step);

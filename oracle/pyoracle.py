@@ -21,7 +21,8 @@ FMT_GRAY8, FMT_RGB8, FMT_BGR8 = 0, 1, 2
 class OraParams(C.Structure):
     _fields_ = [("win", C.c_int), ("max_level", C.c_int), ("max_iters", C.c_int),
                 ("eps", C.c_double), ("min_eig", C.c_float), ("thresh", C.c_int),
-                ("pixel_step", C.c_int), ("min_vector_size", C.c_double)]
+                ("pixel_step", C.c_int), ("min_vector_size", C.c_double), ("fit_mode", C.c_int),
+                ("ransac_iters", C.c_int), ("ransac_thresh", C.c_double), ("ransac_seed", C.c_uint32)]
 
 
 MAXL = 16
@@ -69,6 +70,8 @@ def lib():
         L.ora_invert3x3.restype = C.c_int
         L.ora_warp_perspective.argtypes = [u8p, C.c_int, C.c_int, C.c_int, f64p, u8p, C.c_int, C.c_int]
         L.ora_absdiff_threshold.argtypes = [u8p, u8p, C.c_int, C.c_int, u8p]
+        L.ora_fit_ransac.argtypes = [f32p, f32p, C.c_int, C.c_int, C.c_double, C.c_uint32, f64p, C.POINTER(C.c_int)]
+        L.ora_fit_ransac.restype = C.c_int
         L.ora_grid_count.argtypes = [C.c_int, C.c_int, C.c_int]
         L.ora_grid_count.restype = C.c_int
         L.ora_calculate_optical_flow.argtypes = [u8p, u8p, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -161,6 +164,18 @@ def get_perspective_transform(src4: np.ndarray, dst4: np.ndarray) -> np.ndarray:
     M = np.zeros(9)
     lib().ora_get_perspective_transform(_p(s, C.c_float), _p(d, C.c_float), _p(M, C.c_double))
     return M.reshape(3, 3)
+
+
+def fit_ransac(src: np.ndarray, dst: np.ndarray, iters: int = 128, thresh: float = 3.0, seed: int = 20141105):
+    """The product's MDX_FIT_RANSAC restated (ora_fit_ransac; not in the reference).  src, dst: (n, 2)
+    float32 accepted vectors in x-major order.  Returns (H (3, 3), inlier count, best hypothesis)."""
+    s = np.ascontiguousarray(src, dtype=np.float32).reshape(-1, 2)
+    d = np.ascontiguousarray(dst, dtype=np.float32).reshape(-1, 2)
+    H = np.zeros(9)
+    bh = C.c_int(-1)
+    cnt = lib().ora_fit_ransac(_p(s, C.c_float), _p(d, C.c_float), len(s), iters, thresh, seed & 0xFFFFFFFF,
+                               _p(H, C.c_double), C.byref(bh))
+    return H.reshape(3, 3), cnt, bh.value
 
 
 def set_svd_vblas(on: bool) -> None:
