@@ -22,6 +22,20 @@ def bench_stamp(d):
                     pass
     return None
 
+def fallbacks(d):
+    """lk_fallbacks of every profiled bench line (one per pass)."""
+    out = []
+    for f in sorted(glob.glob(os.path.join(d, "p*.json"))):
+        for line in open(f):
+            line = line.strip()
+            if line.startswith("{"):
+                try:
+                    out.append(json.loads(line).get("lk_fallbacks"))
+                except ValueError:
+                    pass
+    return out
+
+
 d = sys.argv[1]
 steps_arg = sys.argv[2] if len(sys.argv) > 2 else "auto"
 tot = defaultdict(float)
@@ -47,7 +61,9 @@ out = {"kernels": "k_lk_class + k_lk_A + k_lk_iter", "config": f"{w}x{h}x{cfg['b
        "sq_insts_lds_per_step": tot["SQ_INSTS_LDS"] / steps,
        "per_kernel_valu_per_step": {k: v["SQ_INSTS_VALU"] / steps for k, v in per_kernel.items()},
        "counters_per_step": {k: v / steps for k, v in sorted(tot.items())},
-       "source": "scripts/pmc_lk.sh (rocprofv3 --pmc, two passes; MDX_LK_FLOW=0: counter collection serializes "
-                 "kernels, so the levels run in sequence -- the same groups and iterations)",
+       "source": "scripts/pmc_lk.sh (rocprofv3 --pmc, two passes, level dataflow ON: where counter collection "
+                 "serializes kernels the waits give up and the levels are recomputed in sequence inside each call "
+                 "(lk_fallbacks below, from the profiled bench line))",
+       "lk_fallbacks": fallbacks(d),
        "src_sha256": bench_stamp(d)}
 print(json.dumps(out, indent=1))

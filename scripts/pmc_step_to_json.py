@@ -57,7 +57,8 @@ res = dict(workload=f"{W}x{H} gray, {B} pairs per step, pixel_step 10 (bench.py 
            hbm_bytes_per_px=round((tot_r + tot_w) / px, 2), algorithmic_bytes_per_px=9.0,
            per_kernel=rows, correction="read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE",
            source=os.path.basename(os.path.normpath(d)),
-           note="collected with MDX_LK_FLOW=0 (counter collection serializes kernels; same work per kernel)")
+           note="level dataflow ON (round 5): where counter collection serializes kernels, the LK waits give up "
+                "and the levels are recomputed in sequence inside each call (see the bench lines' lk_fallbacks)")
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: v for k, v in res.items() if k != "per_kernel"}))
 for r in rows[:15]:
