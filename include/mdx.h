@@ -207,7 +207,9 @@ int mdx_warp_diff_dev(mdx_ctx* ctx, int batch, const uint8_t* d_gray1, const uin
  * frame-1 rows its warp reads beyond the band, so d_img1 must still hold frame 1.  Any other entry
  * that rebuilds the context's pyramids in between (a pair or trajectory call) voids them: step 3
  * then returns MDX_EINVAL instead of warping another pair's frames.  fit_mode must be
- * MDX_FIT_FIRST4.
+ * MDX_FIT_FIRST4.  With call pipelining, consecutive band calls alternate the two pyramid halves;
+ * step 3 reads (and then releases) only the latest call's half, the other half having been
+ * released by its own call once its classification was queued.
  */
 typedef struct mdx_band_cand {
     int32_t count;     /* accepted vectors (status && |d| > min_vector_size) in the band */

@@ -86,6 +86,10 @@ struct mdx_ctx {
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
     int lk_sub = 0;                          // > 0: LK sub-batch cap (MDX_LK_SUB, tests)
     bool lk_arows = true;                    // A sums per row strip where the plan allows (MDX_LK_AROWS=0: per group)
+    bool lk_pflow = false;                   // MDX_LK_PFLOW=1: per-point dataflow even for large batches (A/B)
+    int lk_epoch = 0;                        // per-point dataflow: the last call's epoch
+    void* pflag_mem = nullptr;               // the Abuf allocation and layout whose per-point flags were zeroed
+    size_t pflag_at = 0, pflag_bytes = 0, pflag_per = 0;
     int plan_w = -1, plan_h = -1, plan_ps = -1, plan_ml = -1, plan_gy0 = -1, plan_gy1 = -1;
     int band_w = 0, band_h = 0;              // frame of the last mdx_band_flow_dev (its pyramids are live)
     ClassPlan plan{};
@@ -402,6 +406,7 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     if (const char* e = std::getenv("MDX_LK_G")) c->lk_g = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_SUB")) c->lk_sub = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_AROWS")) c->lk_arows = std::atoi(e) != 0;
+    if (const char* e = std::getenv("MDX_LK_PFLOW")) c->lk_pflow = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_TRAJ_CHAIN")) c->traj_chain = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_TRAJ_PPW")) c->traj_ppw = std::atoi(e) == 1 ? 1 : 2;
@@ -693,11 +698,38 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
     const size_t dbytes = ((size_t)kMaxLevels * batch + kLkFlagInts) * kCtrPad * sizeof(int);
     const size_t lbytes = ((size_t)batch * npts * 8 + 127) / 128 * 128;   // one level's carried points
     const size_t cbytes = lbytes * g.nlev;
-    if ((rc = ensure(c, c->Abuf, abytes + 2 * (qbytes + dbytes + cbytes))) != MDX_OK) return rc;
+    // per-point dataflow flags: [level][pair][point] epochs, per parity (zeroed once per allocation;
+    // every call's epoch exceeds the earlier ones', so stale stamps never satisfy a wait)
+    const size_t fbytes = ((size_t)batch * npts * 4 + 127) / 128 * 128;
+    const size_t pbytes = fbytes * g.nlev;
+    const size_t per = qbytes + dbytes + cbytes + pbytes;
+    if ((rc = ensure(c, c->Abuf, abytes + 2 * per)) != MDX_OK) return rc;
+    // (re)zeroed whenever the flags move: stale bytes of another layout (A sums, carried points)
+    // could read as large epochs
+    const size_t pf_at = abytes + qbytes + dbytes + cbytes;
+    if (c->lk_epoch >= (1 << 30)) {   // epochs wrap: start again from zeroed flags
+        c->lk_epoch = 0;
+        c->pflag_mem = nullptr;
+    }
+    if (c->pflag_mem != c->Abuf.p || c->pflag_at != pf_at || c->pflag_bytes != pbytes || c->pflag_per != per) {
+        // only the flag regions: the aux stream may already write the A sums of this allocation;
+        // the flags' writers and readers (the iteration launches) follow c->stream
+        for (int q = 0; q < 2; q++)
+            HIP_OR_RETURN(c, hipMemsetAsync(c->Abuf.as<uint8_t>() + abytes + q * per + qbytes + dbytes + cbytes, 0,
+                                            pbytes, c->stream));
+        c->pflag_mem = c->Abuf.p;
+        c->pflag_at = pf_at;
+        c->pflag_bytes = pbytes;
+        c->pflag_per = per;
+    }
     const int par = parity < 0 ? 0 : parity;
-    uint8_t* base = c->Abuf.as<uint8_t>() + abytes + par * (qbytes + dbytes + cbytes);
+    uint8_t* base = c->Abuf.as<uint8_t>() + abytes + par * per;
     a.carry = reinterpret_cast<float*>(base + qbytes + dbytes);
     a.carry_lstride = (long long)(lbytes / sizeof(float));
+    a.pflags = reinterpret_cast<int*>(base + qbytes + dbytes + cbytes);
+    a.pf_lstride = (long long)(fbytes / sizeof(int));
+    a.epoch = ++c->lk_epoch;
+    a.pflow_force = c->lk_pflow ? 1 : 0;
     HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
                                   reinterpret_cast<int*>(base), prev_ready, c->iter2, c->flowev,
                                   reinterpret_cast<int*>(base + qbytes), c->prm.call_pipelining ? c->lvl_done : nullptr,

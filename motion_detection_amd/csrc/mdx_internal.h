@@ -119,6 +119,13 @@ struct LkArgs {
                              // the level launches run one after another
     int done_stride;
     int dep_groups;          // > 0: groups per pair of the coarser level, which a group waits for
+    int dep_points;          // 1: per-point dataflow -- a group waits only for its own points' coarser
+                             // level results (pflags), not for the whole pair's level (small batches)
+    int* pflags;             // per-point dataflow: [level][batch][npts] epoch of each point's last
+                             // retirement at that level (this sub-batch's first pair)
+    long long pf_lstride;    // ints between two levels of pflags
+    int epoch;               // this call's epoch (> every earlier call's)
+    int pflow_force;         // 1: per-point dataflow even where the per-pair form applies (MDX_LK_PFLOW)
     int* err;                // dataflow statistics, read and cleared at the context's sync points:
                              // [0] group waits and [1] gate waits that gave up, [2] levels recomputed
     int* lflags;             // dataflow: the call's per-level flags (kLkFlag* below, zeroed with

@@ -807,11 +807,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
         if (a.done && level > 0) {
             // the group's points have their level result: once this wave's stores are done, one
             // lane of the slot counts the group for its pair (MI355X_MICROARCH.md hand-off: sc1
-            // stores, vmcnt(0), agent atomic; the reader polls and loads sc1)
+            // stores, vmcnt(0), agent atomic; the reader polls and loads sc1) -- or, per-point
+            // dataflow, each point's lane stamps the point with the call's epoch
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (sl == 0)
+            if (a.dep_points) {
+                if (q.valid && k == 0)
+                    __hip_atomic_store(a.pflags + level * a.pf_lstride + po, a.epoch, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            } else if (sl == 0) {
                 __hip_atomic_fetch_add(a.done + (level * a.done_stride + pair) * kCtrPad, 1, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     };
 
@@ -847,22 +853,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                     } else {
                         float2 p = make_float2(0.f, 0.f);
                         const float* src = a.carry ? a.carry + (level + 1) * a.carry_lstride : a.next_pts;
-                        if (a.dep_groups) {
+                        const bool wait_pt = a.dep_points && level < a.maxl;
+                        if (a.dep_groups || wait_pt) {
                             // dataflow: the coarser level may still run -- wait until every group of
-                            // this pair has retired there (bounded: its waves are resident and
-                            // drain their queue), then read the carried points past L1.  A wait
-                            // that gives up abandons the level (every later wait sees the flag):
-                            // its groups drain without computing, and its recompute launch
+                            // this pair has retired there (per-point dataflow: until this lane's
+                            // point has; bounded: the coarser level's waves are resident and drain
+                            // their queue), then read the carried points past L1.  A wait that
+                            // gives up abandons the level (every later wait sees the flag): its
+                            // groups drain without computing, and its recompute launch
                             // (launch_lk_v2) runs it again once the coarser level is done.
-                            if (sl == 0 && !gave_up) {
+                            const bool waiter = wait_pt ? (q.valid && k == 0) : (sl == 0);
+                            if (waiter && !gave_up) {
                                 // polls back off (1 .. 16 sleeps between loads): thousands of
                                 // waiting waves polling one line would load its L2 channel
-                                const int* d = a.done + ((level + 1) * a.done_stride + pair) * kCtrPad;
+                                const int* d = wait_pt ? a.pflags + (level + 1) * a.pf_lstride + po
+                                                       : a.done + ((level + 1) * a.done_stride + pair) * kCtrPad;
+                                const int target = wait_pt ? a.epoch : a.dep_groups;
                                 int slept = 0, gap = 1;
                                 bool mine = false;
                                 if (a.spin_max < 0) mine = true;   // fault injection (tests)
                                 while (!mine &&
-                                       __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.dep_groups) {
+                                       __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                                     if (slept >= a.spin_max) {
                                         mine = true;
                                         break;
@@ -898,7 +909,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                     }
                     act = Dinv > 0.f;   // real point, window inside, eigenvalue / determinant tests passed
                     // an abandoned level retires its groups at once (its recompute redoes them)
-                    if (a.dep_groups && __shfl((int)gave_up, slot * LPS)) act = false;
+                    if ((a.dep_groups || a.dep_points) && (__ballot(gave_up) & smask)) act = false;
                     status = (level == 0 && q.valid && !act) ? 0 : 1;
                     nx = npx - HALFW;
                     ny = npy - HALFW;
@@ -1234,6 +1245,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         b.der = a.der + (long long)p * a.g.der_words;
         b.next_pts = a.next_pts + (long long)p * a.npts * 2;
         b.carry = a.carry ? a.carry + (long long)p * a.npts * 2 : nullptr;   // carry_lstride: whole batch
+        b.pflags = a.pflags ? a.pflags + (long long)p * a.npts : nullptr;      // pf_lstride: whole batch
         b.status = a.status + (long long)p * a.npts;
         if (p) b.dbg = nullptr;   // the trace covers the first sub-batch
         uint8_t* bcls = cls + (long long)p * a.plan.bytes_per_pair;
@@ -1289,9 +1301,15 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         // no two pairs' carried points may share a 128-B line; with one pair per XCD (batch 8) the
         // next level can only start once the whole level is done there, and the dataflow measured
         // 1.5% slower than levels in sequence, so it needs at least two
-        const bool flow = aux && s2 && flow_ev && done && redo_ev && a.err && b.carry && nb % 8 == 0 && nb >= 16 &&
-                          a.npts % 16 == 0 && (reinterpret_cast<uintptr_t>(b.next_pts) & 127) == 0 &&
-                          (reinterpret_cast<uintptr_t>(b.carry) & 127) == 0 && (a.carry_lstride % 32) == 0;
+        const bool flow_ok = aux && s2 && flow_ev && done && redo_ev && a.err && b.carry &&
+                             (reinterpret_cast<uintptr_t>(b.carry) & 127) == 0 && (a.carry_lstride % 32) == 0;
+        // per pair (groups wait for their pair's whole coarser level) where every XCD range holds
+        // two or more whole pairs; per point (groups wait for their own points) for small batches
+        // -- a single pair's level would otherwise wait for the coarser level's slowest group
+        const bool flow_pair = flow_ok && !a.pflow_force && nb % 8 == 0 && nb >= 16 && a.npts % 16 == 0 &&
+                               (reinterpret_cast<uintptr_t>(b.next_pts) & 127) == 0;
+        const bool flow_pt = flow_ok && !flow_pair && b.pflags;
+        const bool flow = flow_pair || flow_pt;
         int* lflags = flow ? done + (long long)kMaxLevels * nb * kCtrPad : nullptr;
         // the even levels' stream (the first level's) and the odd levels'; parity 1 swaps them so
         // that this call's first level does not queue behind the previous call's fit / warp on s
@@ -1321,15 +1339,18 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             bl.dep_groups = 0;
             bl.lflags = lflags;
             bl.redo = 0;
-            if (flow && l < a.maxl) {
+            bl.dep_points = flow_pt ? 1 : 0;
+            if (flow_pair && l < a.maxl) {
                 const ClassLevel& Cp = a.plan.lv[l + 1];
                 bl.dep_groups = (Cp.nxp / Cp.G) * a.nyg;
             }
-            if (bl.dep_groups) {   // start in the coarser level's tail, not beside its whole queue
-                const int ng = (C.nxp / C.G) * a.nyg;
-                hipLaunchKernelGGL(k_lk_gate, dim3(1), dim3(64), 0, st, bq + (l + 1) * 8 * kCtrPad,
-                                   (long long)nb * bl.dep_groups, done + (l + 1) * nb * kCtrPad, bl.dep_groups, ng,
-                                   (long long)nb * ng, a.err, a.spin_max, lflags + (kLkFlagGiveup + l) * kCtrPad);
+            if (flow && l < a.maxl) {   // start in the coarser level's tail, not beside its whole queue
+                const ClassLevel& Cp = a.plan.lv[l + 1];
+                const int ngc = (Cp.nxp / Cp.G) * a.nyg, ng = (C.nxp / C.G) * a.nyg;
+                // per point: the coarser queue handed out is the whole condition (dep_groups 0)
+                hipLaunchKernelGGL(k_lk_gate, dim3(1), dim3(64), 0, st, bq + (l + 1) * 8 * kCtrPad, (long long)nb * ngc,
+                                   done + (l + 1) * nb * kCtrPad, bl.dep_groups, ng, (long long)nb * ng, a.err,
+                                   a.spin_max, lflags + (kLkFlagGiveup + l) * kCtrPad);
             }
             const float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             switch (C.G * 1000 + C.UW) {
@@ -1347,6 +1368,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
                     LkArgs br = bl;
                     br.done = nullptr;
                     br.dep_groups = 0;
+                    br.dep_points = 0;
                     br.redo = 1;
                     br.dbg = nullptr;
                     switch (C.G * 1000 + C.UW) {
