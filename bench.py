@@ -443,6 +443,7 @@ def main_c4(args, D: Dist, threads: int):
         "phase_ms_per_step_rank0": {k: round(v / args.steps * 1e3, 3) for k, v in t_ph.items()},
         "one_band_ms": round(band_ms, 3) if band_ms else None,
         "num_vectors": int(num[0]),
+        "lk_fallbacks": [c.lk_fallbacks() for c in ctxs],
         "roofline": None,
         "cpu_baseline": None,
     }

@@ -273,6 +273,8 @@ class Context:
     def lk_fallbacks(self) -> dict:
         """LK level-dataflow fallbacks since creation, as of the last sync (include/mdx.h
         mdx_lk_fallbacks): waits that gave up and levels recomputed -- statistics, not errors."""
+        if not hasattr(lib(), "mdx_lk_fallbacks"):     # (variant builds of older sources: A/B runs)
+            return None
         v = (C.c_longlong * 3)()
         self._check(lib().mdx_lk_fallbacks(self._h, v))
         return {"group_giveups": v[0], "gate_giveups": v[1], "levels_recomputed": v[2]}
