@@ -86,7 +86,9 @@ struct mdx_ctx {
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
     int lk_sub = 0;                          // > 0: LK sub-batch cap (MDX_LK_SUB, tests)
     bool lk_arows = true;                    // A sums per row strip where the plan allows (MDX_LK_AROWS=0: per group)
-    bool lk_pflow = false;                   // MDX_LK_PFLOW=1: per-point dataflow even for large batches (A/B)
+    // MDX_LK_PFLOW: 1 per-point dataflow wherever the per-pair form does not apply (small batches,
+    // row bands), 2 everywhere; 0 (default) never -- measured slower for row bands
+    int lk_pflow = 0;
     int lk_epoch = 0;                        // per-point dataflow: the last call's epoch
     void* pflag_mem = nullptr;               // the Abuf allocation and layout whose per-point flags were zeroed
     size_t pflag_at = 0, pflag_bytes = 0, pflag_per = 0;
@@ -406,7 +408,7 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     if (const char* e = std::getenv("MDX_LK_G")) c->lk_g = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_SUB")) c->lk_sub = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_AROWS")) c->lk_arows = std::atoi(e) != 0;
-    if (const char* e = std::getenv("MDX_LK_PFLOW")) c->lk_pflow = std::atoi(e) != 0;
+    if (const char* e = std::getenv("MDX_LK_PFLOW")) c->lk_pflow = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_TRAJ_CHAIN")) c->traj_chain = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_TRAJ_PPW")) c->traj_ppw = std::atoi(e) == 1 ? 1 : 2;
@@ -726,10 +728,10 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
     uint8_t* base = c->Abuf.as<uint8_t>() + abytes + par * per;
     a.carry = reinterpret_cast<float*>(base + qbytes + dbytes);
     a.carry_lstride = (long long)(lbytes / sizeof(float));
-    a.pflags = reinterpret_cast<int*>(base + qbytes + dbytes + cbytes);
+    a.pflags = c->lk_pflow <= 0 ? nullptr : reinterpret_cast<int*>(base + qbytes + dbytes + cbytes);
     a.pf_lstride = (long long)(fbytes / sizeof(int));
     a.epoch = ++c->lk_epoch;
-    a.pflow_force = c->lk_pflow ? 1 : 0;
+    a.pflow_force = c->lk_pflow > 1 ? 1 : 0;
     HIP_OR_RETURN(c, launch_lk_v2(s, c->aux, c->lkev, batch, a, c->cls.as<uint8_t>(), c->Abuf.as<float4>(),
                                   reinterpret_cast<int*>(base), prev_ready, c->iter2, c->flowev,
                                   reinterpret_cast<int*>(base + qbytes), c->prm.call_pipelining ? c->lvl_done : nullptr,

@@ -170,6 +170,44 @@ def test_dataflow_fallback_is_bit_exact(mdx, oracle, monkeypatch, spin):
             _check_slot(got[j], i, refs[s], f"spin {spin} call {j} slot {i} seed {s}")
 
 
+@pytest.mark.parametrize("mode,spin,w,h,batch", [("1", None, 1920, 1080, 1), ("1", None, 640, 480, 4),
+                                                  ("2", None, 1920, 1080, 16), ("1", "-1", 640, 480, 4)])
+def test_per_point_dataflow_bit_exact(mdx, oracle, monkeypatch, mode, spin, w, h, batch):
+    """The opt-in per-point level dataflow (MDX_LK_PFLOW=1: batches the per-pair form does not take;
+    2: every batch): a group waits only for its own points' coarser-level results, stamped with the
+    call's epoch.  Two calls back to back (epochs 1 and 2, flags not cleared in between), pipelined;
+    with MDX_LK_SPIN_MAX=-1 every wait gives up and the levels are recomputed.  Bit-exact."""
+    monkeypatch.setenv("MDX_LK_PFLOW", mode)
+    if spin:
+        monkeypatch.setenv("MDX_LK_SPIN_MAX", spin)
+    seeds = [31000 + i for i in range(min(batch, 4))]
+    pairs = _pairs(mdx, seeds, w, h)
+    refs = _oracle_refs(oracle, pairs)
+    slots = [seeds[i % len(seeds)] for i in range(batch)]
+    n = mdx.grid_count(w, h, PS)
+    with mdx.Context(0, w, h, batch, pixel_step=PS, min_vector_size=1.0, call_pipelining=1) as c:
+        g1, g2 = _stack(pairs, slots)
+        d1, d2 = c.dev_alloc(g1.nbytes), c.dev_alloc(g2.nbytes)
+        c.h2d(d1, g1)
+        c.h2d(d2, g2)
+        outs = [_alloc_out(c, n, w, h, batch, vectors=True) for _ in range(2)]
+        for o in outs:
+            _call(c, batch, d1, d2, o, w, h)
+        c.sync()
+        fb = c.lk_fallbacks()
+        got = [_read_out(c, o, n, w, h, batch) for o in outs]
+        for o in outs:
+            for p in o.values():
+                c.dev_free(p)
+        c.dev_free(d1)
+        c.dev_free(d2)
+    if spin:
+        assert fb["levels_recomputed"] > 0
+    for j in range(2):
+        for i, sd in enumerate(slots):
+            _check_slot(got[j], i, refs[sd], f"pflow {mode} call {j} slot {i}")
+
+
 def test_default_run_has_no_fallbacks(mdx, monkeypatch):
     """With the default wait bound on an idle device no wait gives up: the fallback counters stay 0
     over a few pipelined calls (the bench reports the same counters)."""
