@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 S1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS"
 S2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT"
 out=gpurun_out/pmc_lk; mkdir -p $out
-ARGS="--steps 2 --warmup 1 --no-cpu --no-roofline --no-live --no-4k --no-lk-roofline"
+ARGS="--steps 2 --warmup 1 --no-cpu --no-roofline --no-live --no-4k --no-ransac --no-lk-roofline"
 i=0
 for set in "$S1" "$S2"; do
     i=$((i+1))

@@ -23,7 +23,7 @@ else
     step pmc_step
     # dataflow ON (round 5): under counter collection kernels serialize, the waits give up and
     # the levels are recomputed in sequence within each call (lk_fallbacks in the bench line)
-    BENCH_ARGS="--steps 2 --warmup 1 --no-cpu --no-roofline --no-live --no-4k --no-lk-roofline" \
+    BENCH_ARGS="--steps 2 --warmup 1 --no-cpu --no-roofline --no-live --no-4k --no-ransac --no-lk-roofline" \
         bash scripts/pmc_sets.sh step "FETCH_SIZE" "WRITE_SIZE" > $out/pmc_step.log 2>&1 || exit 1
     step pmc_warp
     BENCH_ARGS="--only-roofline --steps 3 --warmup 1 --no-cpu" \
