@@ -536,6 +536,9 @@ def main():
     ap.add_argument("--roofline-config", default="4k", choices=sorted(CONFIGS))
     ap.add_argument("--roofline-batch", type=int, default=32)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--roofline-h", default="both", choices=["both", "affine", "projective"],
+                    help="roofline leg launches: the affine true H, the projective H, or both (profiling passes "
+                         "take one kind at a time so per-launch counters and records stay per kind)")
     ap.add_argument("--only-roofline", action="store_true", help="profiling aid: only the warp+diff roofline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="main CPU-baseline leg (all CPUs, SSE2); the 1-core and scalar legs take half")
     ap.add_argument("--no-cpu", action="store_true")
@@ -748,17 +751,19 @@ def main():
         e1, e2 = rctx.dev_alloc(r1.nbytes), rctx.dev_alloc(r2.nbytes)
         eH, eM = rctx.dev_alloc(Hb.nbytes), rctx.dev_alloc(RB * rw * rh)
         rctx.h2d(e1, r1); rctx.h2d(e2, r2); rctx.h2d(eH, Hb)
-        for _ in range(max(2, args.warmup)):
-            rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
-        rctx.device_sync()
-        rctx.enable_timing(True)
-        for _ in range(args.steps):
-            rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
-        rctx.device_sync()
-        rs = rctx.stage_ms()
-        launch_ms = rs["warp_diff"] / max(rs["calls"], 1)
+        launch_ms = None
+        if args.roofline_h != "projective":
+            for _ in range(max(2, args.warmup)):
+                rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
+            rctx.device_sync()
+            rctx.enable_timing(True)
+            for _ in range(args.steps):
+                rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
+            rctx.device_sync()
+            rs = rctx.stage_ms()
+            launch_ms = rs["warp_diff"] / max(rs["calls"], 1)
         alg_bytes = 3.0 * RB * rw * rh     # read gray1 + read gray2 + write mask, 1 B/px each
-        achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
+        achieved = alg_bytes / (launch_ms * 1e-3) / 1e9 if launch_ms else None
         # the memory ceiling of this access mix: the same 3 B/px as one linear non-temporal pass
         # (mdx_probe_stream3_dev, same buffers, same event bracketing)
         for _ in range(2):
@@ -771,35 +776,46 @@ def main():
         cs = rctx.stage_ms()
         copy_ms = cs["warp_diff"] / max(cs["calls"], 1)
         copy_gbs = alg_bytes / (copy_ms * 1e-3) / 1e9
+        kt = stamped_pmc(os.path.join(ROOT, "profiles", "warp_kernel_trace.json"), "config", f"{rw}x{rh}x{RB}")
         # the same launch with a projective H (every non-degenerate first-4 fit is projective): the
         # tests' perspective matrix (tests/test_warp_gpu.py "projective"), per-pixel W and 32 / W
         Hp = np.array([[1.002, 0.013, -2.5], [-0.011, 0.995, 1.75], [2.1e-5, -1.3e-5, 1.0]])
-        rctx.h2d(eH, np.ascontiguousarray(np.broadcast_to(Hp, (RB, 3, 3)), dtype=np.float64))
-        for _ in range(2):
-            rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
-        rctx.device_sync()
-        rctx.enable_timing(True)
-        for _ in range(args.steps):
-            rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
-        rctx.device_sync()
-        ps_ = rctx.stage_ms()
-        proj_ms = ps_["warp_diff"] / max(ps_["calls"], 1)
-        proj_gbs = alg_bytes / (proj_ms * 1e-3) / 1e9
-        projective = dict(avg_launch_us=round(proj_ms * 1e3, 2), achieved=round(proj_gbs, 1),
-                          frac=round(proj_gbs / HBM_PEAK_GBS, 4), launch_over_affine=round(proj_ms / launch_ms, 3),
-                          H=Hp.ravel().tolist(),
-                          workload=f"{rw}x{rh} gray, {RB} pairs per launch, projective H (M6, M7 != 0)")
+        projective = None
+        if args.roofline_h != "affine":
+            rctx.h2d(eH, np.ascontiguousarray(np.broadcast_to(Hp, (RB, 3, 3)), dtype=np.float64))
+            for _ in range(2):
+                rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
+            rctx.device_sync()
+            rctx.enable_timing(True)
+            for _ in range(args.steps):
+                rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
+            rctx.device_sync()
+            ps_ = rctx.stage_ms()
+            proj_ms = ps_["warp_diff"] / max(ps_["calls"], 1)
+            proj_gbs = alg_bytes / (proj_ms * 1e-3) / 1e9
+            pkt = stamped_pmc(os.path.join(ROOT, "profiles", "warp_kernel_trace_projective.json"), "config",
+                              f"{rw}x{rh}x{RB}")
+            projective = dict(avg_launch_us=round(proj_ms * 1e3, 2), achieved=round(proj_gbs, 1),
+                              frac=round(proj_gbs / HBM_PEAK_GBS, 4),
+                              launch_over_affine=round(proj_ms / launch_ms, 3) if launch_ms else None,
+                              H=Hp.ravel().tolist(),
+                              workload=f"{rw}x{rh} gray, {RB} pairs per launch, projective H (M6, M7 != 0)",
+                              kernel_trace=({k: pkt[k] for k in ("launch", "k_warp_diff", "k_warp_prep", "source")
+                                             if k in pkt} if pkt else None))
+            if pkt and kt:
+                projective["kernel_trace_launch_over_affine"] = round(
+                    pkt["launch"]["avg_us"] / kt["launch"]["avg_us"], 3) if "avg_us" in pkt.get("launch", {}) else None
         pmc = stamped_pmc(args.pmc_json, "config", f"{rw}x{rh}x{RB}")
         traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-        kt = stamped_pmc(os.path.join(ROOT, "profiles", "warp_kernel_trace.json"), "config", f"{rw}x{rh}x{RB}")
-        roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, kernel="k_warp_diff",
+        roof = dict(bound="hbm", achieved=round(achieved, 1) if achieved else None, peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(achieved / HBM_PEAK_GBS, 4) if achieved else None, traffic=traffic, kernel="k_warp_diff",
                     workload=f"{rw}x{rh} gray, {RB} pairs per launch, true H (affine), 3 B/px algorithmic",
-                    avg_launch_us=round(launch_ms * 1e3, 2), algorithmic_bytes_per_launch=int(alg_bytes),
+                    avg_launch_us=round(launch_ms * 1e3, 2) if launch_ms else None,
+                    algorithmic_bytes_per_launch=int(alg_bytes),
                     copy_ceiling=dict(achieved=round(copy_gbs, 1), avg_launch_us=round(copy_ms * 1e3, 2),
                                       what="linear 3 B/px pass, 16 B/lane, non-temporal (k_stream3)"),
                     copy_ceiling_frac=round(copy_gbs / HBM_PEAK_GBS, 4),
-                    frac_of_copy_ceiling=round(achieved / copy_gbs, 4),
+                    frac_of_copy_ceiling=round(achieved / copy_gbs, 4) if achieved else None,
                     kernel_trace=({k: kt[k] for k in ("launch", "k_warp_diff", "k_warp_prep", "k_stream3",
                                                        "frac_of_copy_ceiling", "source") if k in kt}
                                   if kt else None),

@@ -155,7 +155,10 @@ constexpr int kLkFlagQueue = 2 * kMaxLevels;
 constexpr int kLkFlagInts = kLkFlagQueue + 8 * kMaxLevels;
 // persistent waves of a recompute launch: cheap when it exits at once (the common case), and a
 // recompute of the finest level at 1080p x 32 still takes only tens of ms
-constexpr int kLkRedoWaves = 512;
+#ifndef MDX_LK_REDO_WAVES
+#define MDX_LK_REDO_WAVES 512
+#endif
+constexpr int kLkRedoWaves = MDX_LK_REDO_WAVES;
 
 // Core rows [lo, hi) of one pyramid level (row-band mode: what a band's LK reads)
 struct RowSpan {

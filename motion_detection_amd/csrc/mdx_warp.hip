@@ -43,8 +43,8 @@
 // Projective M (M6 or M7 != 0, e.g. every non-degenerate first-4 fit) takes the same tiles: the
 // tile's footprint is the bounding box of its reference blocks' corner images (the homography maps
 // the tile to a convex quadrilateral when W keeps one sign over it) widened by one pixel for the
-// rounding of interior pixels, and each pixel evaluates the reference's W = W0 + M6*x1, the
-// correctly rounded 32/W and its own rounded products (warp_rows<.., PROJ = true>).
+// rounding of interior pixels; each pixel's coordinates come from a cheap estimate of the quotient,
+// settled with the reference's exact expression when it lies near a rounding boundary (warp_rows_pj).
 // Everything else (W changing sign over a tile, small frames, huge or far-away footprints) takes
 // the general per-pixel path, exact for any input.
 #include "mdx_internal.h"
@@ -136,11 +136,12 @@ __device__ TileInfo tile_info(const double* M, int x0, int y0, int w, int yend, 
         const double Wv = W0 + M[6] * x1;
         Wd = Wv != 0.0 ? 32.0 / Wv : 0.0;
         const double aw = fabs(Wv);
-        // W in [2^-100, 2^100] at every corner (so over the tile): div32's range
-        wsign = (aw >= 0x1p-100 && aw <= 0x1p100) ? (Wv > 0.0 ? 1 : 2) : 0;
+        // W in [2^-100, 2^100] at every corner (so over the tile): div32's range; |W| >= 64 |M6|:
+        // W0 + M6 * x1 does not cancel (warp_rows_pj's estimate)
+        wsign = (aw >= 0x1p-100 && aw <= 0x1p100 && aw >= 64.0 * fabs(M[6])) ? (Wv > 0.0 ? 1 : 2) : 0;
     }
     const double px = (X0 + M[0] * x1) * Wd, py = (Y0 + M[3] * x1) * Wd;
-    const double lim = 1073741824.0;   // 2^30
+    const double lim = affine ? 1073741824.0 : 16777216.0;   // 2^30; projective 2^24 (warp_rows_pj's bound)
     int ok = (px > -lim && px < lim && py > -lim && py < lim && wsign != 0) ? 1 : 0;
     int smin = wsign, smax = wsign;
     int sx = 0, sy = 0;
@@ -200,7 +201,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, lon
 // without, 230-234 with nt on the footprint too, 222-224 with nt on the mask only; on a second box
 // 211-220 with nt against 223-229 without.
 constexpr int kCpStream = 2;   // buffer aux bit 1 = nt
-typedef __attribute__((address_space(3))) const double lds_d1;
 // 32 / d correctly rounded, for |d| in [2^-100, 2^100] (tile_info keeps the fast path there): the
 // compiler's IEEE double division without its v_div_scale / v_div_fixup steps, which only act on
 // exponents far outside that range (huge quotients, denormals, inf / nan) -- two Newton steps on
@@ -218,15 +218,11 @@ __device__ __forceinline__ double div32(double d)
     const double rem = __builtin_fma(-d, q0, 32.0);
     return __builtin_fma(rem, r2, q0);
 }
-// PROJ: projective M -- per pixel W = W0 + fl(M6*x1) (W0 per row and block from wp, tw[k] = fl(M6*x1)),
-// Wd = 32 / W correctly rounded (the reference's W ? 32/W : 0; nonzero on the fast path), and the
-// product (X0 + M0*x1) * Wd rounded before the magic add rounds it to an integer, as in the reference
-template <bool POW2, bool ROWCHK, bool PROJ = false>
+template <bool POW2, bool ROWCHK>
 __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t src_base, int nvalid,
                                           __amdgpu_buffer_rsrc_t g2rs, uint32_t g2off, int g2s,
                                           __amdgpu_buffer_rsrc_t mrs, uint32_t moff, int ms, const double* tx,
-                                          const double* ty, double Wd, double mX, double mY, uint32_t bias,
-                                          lds_d1* wp = nullptr, const double* tw = nullptr)
+                                          const double* ty, double Wd, double mX, double mY, uint32_t bias)
 {
     uint32_t G[kTH / 8];
 #pragma unroll
@@ -235,19 +231,12 @@ __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t sr
     for (int i = 0; i < kTH / 8; i++) {
         const int ri = ROWCHK ? (i < nvalid ? i : 0) : i;
         const d2v xy = xyp[16 * ri];                      // rows are 2 blocks x 16 B apart
-        double w0 = 0.0;
-        if constexpr (PROJ) w0 = wp[16 * ri];             // rows are 2 blocks x 8 B apart
         uint32_t xs_[4], ys_[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const double ax = xy.x + tx[k], ay = xy.y + ty[k];
             double rx, ry;
-            if constexpr (PROJ) {
-                const double Wv = w0 + tw[k];
-                const double Wk = div32(Wv);              // = 32.0 / Wv (|Wv| in [2^-100, 2^100] on a fast tile)
-                rx = ax * Wk + mX;
-                ry = ay * Wk + mY;
-            } else if (POW2) {                            // (X0 + M0*x1) * Wd exact: one rounding
+            if (POW2) {                            // (X0 + M0*x1) * Wd exact: one rounding
                 rx = __builtin_fma(ax, Wd, mX);
                 ry = __builtin_fma(ay, Wd, mY);
             } else {                                      // round the product, then to integer
@@ -376,6 +365,106 @@ __device__ __forceinline__ void warp_rows_fx(lds_u4* fxp, lds_d2* xyp, uint32_t 
     }
 }
 
+// Projective rows.  The reference's X = cvRound(fl(fl(X0 + fl(M0*x1)) * fl(32 / fl(W0 + fl(M6*x1))))) is
+// taken in two steps.  First an estimate, in warp_rows_fx's fixed-point layout relative to the
+// staged origin (U = [ staged column (8 bits) | fx (5 bits) | fraction (19 bits) ], U ~ 2^19 (X' + 1/2)):
+// r ~ 2^24 / W from v_rcp_f64 and one cubic Newton step (rcp's relative error e -> e^3, about
+// 2^-69, plus the step's own roundings, ~2^-52), then U = RN(ax * r + 2^18 - 2^24 sxa), one FMA
+// per axis.  The estimate's operands need not be the reference's roundings: ax and W / 2^24 of
+// column x1b + k come from the lane's column x1b by k more FMAs (ax = fl(M0 * k + fl(X0 + M0 * x1b))),
+// so no per-column table is held in registers.  tile_info keeps projective fast tiles at |X|, |Y| <
+// 2^24 (1/32 px units) and |W| >= 64 |M6| at the corners (no cancellation in W0 + M6 * x1), so the
+// estimate and the reference each stay within 2^24 * 2^19 * 2^-49 = 1/64 unit of 2^-19 of the exact
+// quotient: whenever U's fraction is at least kPjGuard units from the boundary (0), floor(U / 2^19)
+// is the reference's X' and not a tie.  The other pixels (64 of every 2^19 fractions per axis) take
+// the exact form: W, the correctly rounded 32/W (div32) and the rounded product.  Then the taps,
+// weights and threshold are warp_rows_fx's.
+constexpr uint32_t kPjGuard = 32;
+__device__ __forceinline__ bool pj_near(uint32_t u)
+{
+    return ((u + kPjGuard) & 0x7ffffu) < 2 * kPjGuard;
+}
+__device__ __forceinline__ void warp_rows_pj(lds_d2* xyp, lds_d2* wpp, uint32_t src_base, int nvalid,
+                                             __amdgpu_buffer_rsrc_t g2rs, uint32_t g2off, int g2s,
+                                             __amdgpu_buffer_rsrc_t mrs, uint32_t moff, int ms, double tx0, double ty0,
+                                             double tws0, const double* M, int x1b, double mX, double mY, double mXs,
+                                             double mYs, uint32_t bias)
+{
+    uint32_t G[kTH / 8];
+#pragma unroll
+    for (int i = 0; i < kTH / 8; i++) G[i] = __builtin_amdgcn_raw_buffer_load_b32(g2rs, (int)g2off, i * g2s, kCpStream);
+    uint32_t gsel[4], mulx;
+    asm volatile("s_mov_b32 %0, 0x0c000c0c" : "=s"(gsel[0]));
+    asm volatile("s_mov_b32 %0, 0x0c010c0c" : "=s"(gsel[1]));
+    asm volatile("s_mov_b32 %0, 0x0c020c0c" : "=s"(gsel[2]));
+    asm volatile("s_mov_b32 %0, 0x0c030c0c" : "=s"(gsel[3]));
+    asm volatile("v_mov_b32 %0, 0x3fffc0" : "=v"(mulx));    // 64 * 65535
+    const double M6s = M[6] * 0x1p-24;
+#pragma unroll
+    for (int i = 0; i < kTH / 8; i++) {
+        const int ri = i < nvalid ? i : 0;                // rows past the band: row r0's coordinates
+        const d2v xy = xyp[16 * ri];                      // (X0, Y0) of this lane's row and block
+        const d2v wv = wpp[16 * ri];                      // (W0, W0 / 2^24)
+        const double ax0 = xy.x + tx0, ay0 = xy.y + ty0, ws0 = wv.y + tws0;
+        uint32_t ux[4], uy[4];
+        uint32_t fmin = 0xffffffffu;                      // the smallest guard-shifted fraction
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const double kd = (double)k;
+            const double ax = k ? __builtin_fma(M[0], kd, ax0) : ax0;
+            const double ay = k ? __builtin_fma(M[3], kd, ay0) : ay0;
+            const double Ws = k ? __builtin_fma(M6s, kd, ws0) : ws0;   // ~ W / 2^24
+            const double r0 = __builtin_amdgcn_rcp(Ws);
+            const double e = __builtin_fma(-Ws, r0, 1.0);
+            const double r = __builtin_fma(r0, __builtin_fma(e, e, e), r0);
+            ux[k] = (uint32_t)__double2loint(__builtin_fma(ax, r, mXs));
+            uy[k] = (uint32_t)__double2loint(__builtin_fma(ay, r, mYs));
+            fmin = min(fmin, min((ux[k] + kPjGuard) & 0x7ffffu, (uy[k] + kPjGuard) & 0x7ffffu));
+        }
+        if (fmin < 2 * kPjGuard) {
+            // within the guard of a rounding boundary (or on a tie): the reference's expression
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t uxk = ux[k], uyk = uy[k];
+                asm volatile("" : "+v"(uxk), "+v"(uyk));   // tested here, per pixel, only on this rare path
+                if (pj_near(uxk) || pj_near(uyk)) {
+                    const double x1 = (double)(x1b + k);
+                    const double Wk = div32(wv.x + M[6] * x1);   // 32 / W, correctly rounded
+                    ux[k] = (uint32_t)__double2loint((xy.x + M[0] * x1) * Wk + mX) << 19;
+                    uy[k] = (uint32_t)__double2loint((xy.y + M[3] * x1) * Wk + mY) << 19;
+                }
+            }
+        }
+        uint32_t ad[4], wys[4], wxs[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            ad[k] = src_base + __builtin_amdgcn_perm(uy[k], ux[k], 0x0c0c0703u);   // (row << 8) | col
+            const uint32_t fx = __builtin_amdgcn_ubfe(ux[k], 19, 5), fy = __builtin_amdgcn_ubfe(uy[k], 19, 5);
+            wys[k] = __umul24(fy, 65535u) + 32u;               // (32 - fy, fy)
+            wxs[k] = __umul24(fx, mulx) + 2048u;               // 64 * (32 - fx, fx)
+        }
+        uint32_t c0s[4], c1s[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            lds_u8* p = (lds_u8*)(uintptr_t)ad[k];
+            c0s[k] = (uint32_t)p[0] | ((uint32_t)p[1] << 16);
+            c1s[k] = (uint32_t)p[kSP] | ((uint32_t)p[kSP + 1] << 16);
+        }
+        uint32_t e[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const u16x2v c0 = __builtin_bit_cast(u16x2v, c0s[k]), c1 = __builtin_bit_cast(u16x2v, c1s[k]);
+            const u16x2v wy = __builtin_bit_cast(u16x2v, wys[k]);
+            const u16x2v q = c0 * wy.xx + c1 * wy.yy;
+            const uint32_t s = __builtin_amdgcn_udot2(q, __builtin_bit_cast(u16x2v, wxs[k]), 32u, false);
+            const uint32_t g16 = __builtin_amdgcn_perm(0u, G[i], gsel[k]);
+            asm("v_sad_u32 %0, %1, %2, %3" : "=v"(e[k]) : "v"(s), "v"(g16), "s"(bias));
+        }
+        const uint32_t out = __builtin_amdgcn_perm(e[1], e[0], 0x0c0c0b09u) | __builtin_amdgcn_perm(e[3], e[2], 0x0b090c0cu);
+        __builtin_amdgcn_raw_buffer_store_b32(out, mrs, (int)moff, i * ms, kCpStream);
+    }
+}
+
 // footprint chunks that cross the image's left / right edge: byte by byte, 0 outside (kept out of
 // line so its per-byte bounds are not computed on the interior path)
 __device__ __noinline__ void stage_edge_chunks(const uint8_t* src, int pitch, int w, int h, int sya, int sx, int ro,
@@ -465,7 +554,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[64];             // weight table (FP64 rows)
     __shared__ __attribute__((aligned(16))) double s_xy[kTH][2][2];         // (X0, Y0) per row, block
-    __shared__ __attribute__((aligned(16))) double s_w0[kTH][2];            // projective: W0 per row, block
+    __shared__ __attribute__((aligned(16))) double s_w0[kTH][2][2];         // projective: (W0, W0 / 2^24) per row, block
     __shared__ __attribute__((aligned(16))) uint8_t s_src[kSH * kSP];
     __shared__ __attribute__((aligned(16))) uint4 s_fx[kTH][2];             // fixed point: (A_x, A_y, flag)
 
@@ -482,7 +571,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     }
     const int pair = bid / (nbx * nby), tile = bid - pair * (nbx * nby);
     const int tx_ = tile % nbx, ty_ = tile / nbx;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // wave index in an SGPR: the staging loop's trip count and LDS addresses stay scalar
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int x0 = tx_ * kTW, y0 = row0 + ty_ * kTH;
     const int cq = lane & 31;
     const int xs = x0 + 4 * cq;                     // this lane's 4 columns
@@ -523,7 +613,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     const double Wd = t.wd;
     // 32/M8 a power of two -> (X0 + M0*x1) * Wd is exact: the fixed-point rows (warp_rows_fx)
     const bool pow2 = affine && Wd != 0.0 && (__double_as_longlong(Wd) & 0x000fffffffffffffLL) == 0;
-    if (!pow2 && tid < 32) {
+    if (affine && !pow2 && tid < 32) {
         s_tab[2 * tid] = (uint32_t)(32 - tid) | ((uint32_t)tid << 16);
         s_tab[2 * tid + 1] = (uint32_t)(64 * (32 - tid)) | ((uint32_t)(64 * tid) << 16);
     }
@@ -573,7 +663,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         const double Y0 = M[3] * xb + M[4] * y + M[5];
         s_xy[r][b][0] = X0;
         s_xy[r][b][1] = Y0;
-        if (!affine) s_w0[r][b] = M[6] * xb + M[7] * y + M[8];
+        if (!affine) {
+            const double W0 = M[6] * xb + M[7] * y + M[8];
+            s_w0[r][b][0] = W0;
+            s_w0[r][b][1] = W0 * 0x1p-24;
+        }
         if (pow2) {
             const double fx_scale = 524288.0;                        // 2^19
             const uint32_t Ax = floor_lo((Wd * X0 + 0.5 - 32.0 * t.sxa) * fx_scale);
@@ -625,17 +719,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         warp_rows<false, true>(xyp, tabp, src_base, nvalid, g2rs, g2off, 8 * g2_pitch, mrs, moff, 8 * w, tx, ty, Wd, mX,
                                mY, bias);
     } else {
-        double tx[4], ty[4], tw[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            tx[k] = M[0] * (x1b + k);
-            ty[k] = M[3] * (x1b + k);
-            tw[k] = M[6] * (x1b + k);
-            asm volatile("" : "+v"(tx[k]), "+v"(ty[k]), "+v"(tw[k]));
-        }
-        lds_d1* wp = (lds_d1*)(&s_w0[r0][blk]);
-        warp_rows<false, true, true>(xyp, tabp, src_base, nvalid, g2rs, g2off, 8 * g2_pitch, mrs, moff, 8 * w, tx, ty,
-                                     0.0, mX, mY, bias, wp, tw);
+        const double x1d = (double)x1b;
+        double tx0 = M[0] * x1d, ty0 = M[3] * x1d, tws0 = (M[6] * x1d) * 0x1p-24;
+        asm volatile("" : "+v"(tx0), "+v"(ty0), "+v"(tws0));   // held in registers across the rows
+        const double mXs = magic + 262144.0 - 16777216.0 * t.sxa, mYs = magic + 262144.0 - 16777216.0 * t.sya;
+        warp_rows_pj((lds_d2*)(&s_xy[r0][blk][0]), (lds_d2*)(&s_w0[r0][blk][0]), src_base, nvalid, g2rs, g2off,
+                     8 * g2_pitch, mrs, moff, 8 * w, tx0, ty0, tws0, M, x1b, mX, mY, mXs, mYs, bias);
     }
 }
 
