@@ -86,6 +86,7 @@ struct mdx_ctx {
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
     int lk_sub = 0;                          // > 0: LK sub-batch cap (MDX_LK_SUB, tests)
     bool lk_arows = true;                    // A sums per row strip where the plan allows (MDX_LK_AROWS=0: per group)
+    int lk_astrip = 0;                       // grid rows per A-sum strip (MDX_LK_ASTRIP; 0: kAStripRows)
     // MDX_LK_PFLOW: 1 per-point dataflow wherever the per-pair form does not apply (small batches,
     // row bands), 2 everywhere; 0 (default) never -- measured slower for row bands
     int lk_pflow = 0;
@@ -329,9 +330,15 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
                     if (d != asp) uniform = false;
                     e++;
                 }
-                for (size_t s = i; s < e; s += kAStripRows) {
+                // small-batch contexts (C4 row bands: one pair per call) take short strips: more
+                // waves in flight for the few pairs' A sums, which then finish sooner (one band
+                // 1.196-1.197 against 1.217-1.226 ms at 16, profiles/r05_ab_astrip.txt); at batch 32
+                // 4..16 rows measured within noise
+                const size_t srows = c->lk_astrip > 0 ? (size_t)c->lk_astrip
+                                                      : (size_t)(c->max_batch <= 4 ? 4 : kAStripRows);
+                for (size_t s = i; s < e; s += srows) {
                     strips.push_back((int16_t)(s - r0));
-                    strips.push_back((int16_t)std::min<size_t>(kAStripRows, e - s));
+                    strips.push_back((int16_t)std::min<size_t>(srows, e - s));
                 }
                 i = e;
             }
@@ -408,6 +415,7 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     if (const char* e = std::getenv("MDX_LK_G")) c->lk_g = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_SUB")) c->lk_sub = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_AROWS")) c->lk_arows = std::atoi(e) != 0;
+    if (const char* e = std::getenv("MDX_LK_ASTRIP")) c->lk_astrip = std::max(0, std::min(std::atoi(e), 64));
     if (const char* e = std::getenv("MDX_LK_PFLOW")) c->lk_pflow = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_TRAJ_CHAIN")) c->traj_chain = std::atoi(e) != 0;

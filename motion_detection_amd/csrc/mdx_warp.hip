@@ -296,7 +296,11 @@ __device__ __forceinline__ void warp_rows(lds_d2* xyp, lds_u8* tab8, uint32_t sr
 // flagged row-blocks test their four pixels.  Then, per pixel: the tap address is byte 3 of the two
 // sums (one v_perm), the bilinear weight pairs come from fx, fy arithmetically (v_bfe + v_mad_u24:
 // f * 65535 + 32 = (32 - f) | f << 16), and the rest is warp_rows's.
-constexpr int kBmBits = 13;                   // bucket map: 2^13 buckets of 64 units per axis
+#ifndef MDX_WARP_BM_BITS
+#define MDX_WARP_BM_BITS 13
+#endif
+constexpr int kBmBits = MDX_WARP_BM_BITS;     // bucket map: 2^kBmBits buckets of 2^(19 - kBmBits) units per axis
+static_assert(kBmBits <= 16, "a bad range (5 units) must span at most two buckets");
 typedef __attribute__((address_space(3))) const v4u lds_u4;
 template <bool ROWCHK>
 __device__ __forceinline__ void warp_rows_fx(lds_u4* fxp, lds_d2* xyp, uint32_t src_base, int nvalid,
