@@ -467,6 +467,15 @@ __global__ __launch_bounds__(256) void k_scharr(const uint8_t* __restrict__ pyr1
 // lane per chain (12 chains for A11/A12/A22, 8 for b1/b2) adds its 80 terms of the chunk in
 // order.  The result is bit-identical to the x86 reference, not merely within tolerance.
 typedef short s2k __attribute__((ext_vector_type(2)));
+// v_dot2_i32_i16 (VOP3P) with its accumulator in an SGPR.  The builtin with a constant accumulator
+// compiles to v_mov + v_dot2c_i32_i16 (the constant rematerialised in a VGPR per dot product): one
+// more VALU per chain (the trajectory LK's rounding biases 256 and 8192).
+__device__ __forceinline__ int sdot2_sacc(s2k a, s2k b, int c)
+{
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
 
 // k_lk<LPP, true>: the chained trajectory passes (TrajChain); grid = nimg-1 passes x npts points,
 // pass-major, one point per wave.
@@ -671,14 +680,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
                             t0 = tap_pair(i0w, i);
                             t1 = tap_pair(i1w, i);
                         }
-                        ival = __builtin_amdgcn_sdot2(t0, W0, __builtin_amdgcn_sdot2(t1, W1, 256, false), false) >> 9;
+                        ival = __builtin_amdgcn_sdot2(t0, W0, sdot2_sacc(t1, W1, 256), false) >> 9;
                         d00 = dr0[i]; d01 = dr0[i + 1]; d10 = dr1[i]; d11 = dr1[i + 1];
                         const s2k x0 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(d01, d00, 0x05040100u));
                         const s2k x1 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(d11, d10, 0x05040100u));
                         const s2k y0 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(d01, d00, 0x07060302u));
                         const s2k y1 = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(d11, d10, 0x07060302u));
-                        ixv = __builtin_amdgcn_sdot2(x0, W0, __builtin_amdgcn_sdot2(x1, W1, 8192, false), false) >> 14;
-                        iyv = __builtin_amdgcn_sdot2(y0, W0, __builtin_amdgcn_sdot2(y1, W1, 8192, false), false) >> 14;
+                        ixv = __builtin_amdgcn_sdot2(x0, W0, sdot2_sacc(x1, W1, 8192), false) >> 14;
+                        iyv = __builtin_amdgcn_sdot2(y0, W0, sdot2_sacc(y1, W1, 8192), false) >> 14;
                     } else {
                         ival = (ip[0] * w00 + ip[1] * w01 + ip[pitch] * w10 + ip[pitch + 1] * w11 + 256) >> 9;
                         d00 = dp[0]; d01 = dp[1]; d10 = dp[pitch]; d11 = dp[pitch + 1];
@@ -788,7 +797,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
                                 t1 = tap_pair(j1w, i);
                             }
                             const s2k W0 = {(short)v00, (short)v01}, W1 = {(short)v10, (short)v11};
-                            jv = __builtin_amdgcn_sdot2(t0, W0, __builtin_amdgcn_sdot2(t1, W1, 256, false), false) >> 9;
+                            jv = __builtin_amdgcn_sdot2(t0, W0, sdot2_sacc(t1, W1, 256), false) >> 9;
                         } else {
                             const uint8_t* jp = Jb + (jbase + c * R * pitch + toff[i]);
                             jv = (jp[0] * v00 + jp[1] * v01 + jp[pitch] * v10 + jp[pitch + 1] * v11 + 256) >> 9;
