@@ -81,7 +81,7 @@ struct mdx_ctx {
     int ring_cap = 0, ring_w = 0, ring_h = 0, ring_ml = -1;
     bool lk_debug = false;
     bool traj_chain = true;                  // trajectory passes in one launch (MDX_TRAJ_CHAIN=0: per pass)
-    int traj_ppw = 2;                        // trajectory LK points per wave (MDX_TRAJ_PPW: 1 or 2)
+    int traj_ppw = 4;                        // trajectory LK points per wave (MDX_TRAJ_PPW: 1, 2 or 4)
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
     int lk_sub = 0;                          // > 0: LK sub-batch cap (MDX_LK_SUB, tests)
@@ -419,7 +419,7 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     if (const char* e = std::getenv("MDX_LK_PFLOW")) c->lk_pflow = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_DEBUG")) c->lk_debug = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_TRAJ_CHAIN")) c->traj_chain = std::atoi(e) != 0;
-    if (const char* e = std::getenv("MDX_TRAJ_PPW")) c->traj_ppw = std::atoi(e) == 1 ? 1 : 2;
+    if (const char* e = std::getenv("MDX_TRAJ_PPW")) c->traj_ppw = std::atoi(e) == 1 ? 1 : std::atoi(e) == 2 ? 2 : 4;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         g_create_err = "hipStreamCreate failed";
         delete c;

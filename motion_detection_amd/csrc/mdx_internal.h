@@ -200,7 +200,7 @@ struct TrajChain {
     int* num;                            // [0] num_vectors, [1] hand-off waits that timed out
     double mvs;                          // min_vector_size
 };
-// ppw: points per wave (1: 64 lanes per point, 2: 32 lanes per point)
+// ppw: points per wave (1: 64 lanes per point, 2: 32, 4: 16)
 hipError_t launch_lk_chain(hipStream_t s, const LkArgs& a, const TrajChain& t, int ppw);
 // Trajectory subspace RANSAC (fitSubspace): mean-subtracted data, nhyp hypotheses of d columns
 // (cols: [nhyp][d]), winner's residuals / outlier flags; best[0] = winner or -1.  Scratch: data

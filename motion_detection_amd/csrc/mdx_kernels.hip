@@ -496,9 +496,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
     constexpr float FLT_SCALE = 1.f / (1 << 20);
     __shared__ float4 lds4[PPW * PT_FLOATS / 4];
 
-    static_assert(!CHAIN || LPP == 64 || LPP == 32, "chain mode: one or two points per wave");
+    static_assert(!CHAIN || LPP == 64 || LPP == 32 || LPP == 16, "chain mode: one, two or four points per wave");
     // row runs: lane s owns RUN adjacent window columns of one row per chunk
-    constexpr int RUN = LPP == 64 ? 5 : LPP == 32 ? 10 : 0;
+    constexpr int RUN = LPP == 64 ? 5 : LPP == 32 ? 10 : LPP == 16 ? 20 : 0;
+    constexpr int RW = (RUN + 1 + 3) / 4;      // words of a realigned run (taps x .. x + RUN)
     const int lane = threadIdx.x;
     const int p = lane / LPP, s = lane % LPP;
     // chain mode: block b = pass * nbp + points (dispatch order: every block a wave waits for was
@@ -540,11 +541,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
         w[1] = __builtin_amdgcn_alignbyte(v.z, v.y, o);
         w[2] = __builtin_amdgcn_alignbyte(v.w, v.z, o);
     };
+    // 28 bytes of a row from byte address p, realigned: w[0..5] = bytes p .. p+23 (runs of 20)
+    auto row24 = [](const uint8_t* p, uint32_t (&w)[6]) {
+        const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+        const u4a4k v = *reinterpret_cast<const u4a4k*>(u & ~(uintptr_t)3);
+        const u3a4k x = *reinterpret_cast<const u3a4k*>((u & ~(uintptr_t)3) + 16);
+        const uint32_t o = (uint32_t)(u & 3);
+        w[0] = __builtin_amdgcn_alignbyte(v.y, v.x, o);
+        w[1] = __builtin_amdgcn_alignbyte(v.z, v.y, o);
+        w[2] = __builtin_amdgcn_alignbyte(v.w, v.z, o);
+        w[3] = __builtin_amdgcn_alignbyte(x.x, v.w, o);
+        w[4] = __builtin_amdgcn_alignbyte(x.y, x.x, o);
+        w[5] = __builtin_amdgcn_alignbyte(x.z, x.y, o);
+    };
     // (byte i, byte i + 1) of a realigned run as a 16-bit pair
     // (i is a constant once the element loops are unrolled)
-    auto tap_pair = [](const uint32_t (&w)[3], int i) -> s2k {
+    auto tap_pair = [](const uint32_t (&w)[RW > 0 ? RW : 1], int i) -> s2k {
         const unsigned sel = 0x0c000c00u | (unsigned)(i & 3) | ((unsigned)((i & 3) + 1) << 16);
-        const uint32_t hi = (i >> 2) + 1 < 3 ? w[(i >> 2) + 1 < 3 ? (i >> 2) + 1 : 2] : 0u;
+        const uint32_t hi = (i >> 2) + 1 < RW ? w[(i >> 2) + 1 < RW ? (i >> 2) + 1 : RW - 1] : 0u;
         return __builtin_bit_cast(s2k, __builtin_amdgcn_perm(hi, w[i >> 2], sel));
     };
 
@@ -625,8 +639,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
             if (ok) {
                 // LPP 64: the run's I bytes and derivative words of both tap rows, vector loads
                 uint64_t r0 = 0, r1 = 0;
-                uint32_t dr0[RUN == 10 ? 11 : 6] = {}, dr1[RUN == 10 ? 11 : 6] = {};
-                uint32_t i0w[3] = {}, i1w[3] = {};
+                uint32_t dr0[RUN >= 10 ? RUN + 1 : 6] = {}, dr1[RUN >= 10 ? RUN + 1 : 6] = {};
+                uint32_t i0w[RW > 0 ? RW : 1] = {}, i1w[RW > 0 ? RW : 1] = {};
+                if constexpr (LPP == 16) {
+                    const int o = ibase + c * R * pitch + toff[0];
+                    row24(Ib + o, i0w);
+                    row24(Ib + o + pitch, i1w);
+                    const uint32_t* dp = Db + o;
+#pragma unroll
+                    for (int rr = 0; rr < 2; rr++) {
+                        uint32_t* dr = rr ? dr1 : dr0;
+                        const uint32_t* q = dp + rr * pitch;
+#pragma unroll
+                        for (int b = 0; b < 5; b++) {
+                            const u4a4k v = *reinterpret_cast<const u4a4k*>(q + 4 * b);
+                            dr[4 * b] = v.x; dr[4 * b + 1] = v.y; dr[4 * b + 2] = v.z; dr[4 * b + 3] = v.w;
+                        }
+                        dr[20] = q[20];
+                    }
+                }
                 if constexpr (LPP == 32) {
                     const int o = ibase + c * R * pitch + toff[0];
                     row12(Ib + o, i0w);
@@ -771,8 +802,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
             for (int c = 0; c < NCH; c++) {
                 if (act) {
                     uint32_t j0l = 0, j0h = 0, j1l = 0, j1h = 0;
-                    uint32_t j0w[3] = {}, j1w[3] = {};
-                    if constexpr (LPP == 64) {
+                    uint32_t j0w[RW > 0 ? RW : 1] = {}, j1w[RW > 0 ? RW : 1] = {};
+                    if constexpr (LPP == 16) {
+                        const uint8_t* jp = Jb + (jbase + c * R * pitch + toff[0]);
+                        row24(jp, j0w);
+                        row24(jp + pitch, j1w);
+                    } else if constexpr (LPP == 64) {
                         const uint8_t* jp = Jb + (jbase + c * R * pitch + toff[0]);
                         row8(jp, j0l, j0h);
                         row8(jp + pitch, j1l, j1h);
@@ -1752,9 +1787,10 @@ hipError_t launch_traj_init(hipStream_t s, int npts, int ny, int pixel_step, int
 hipError_t launch_lk_chain(hipStream_t s, const LkArgs& a, const TrajChain& t, int ppw)
 {
     const long long blocks = (long long)(t.nimg - 1) * ((a.npts + ppw - 1) / ppw);
-    if (t.nimg < 2 || t.nimg > kMaxTrajImgs || a.npts <= 0 || blocks > 0x7fffffffLL || (ppw != 1 && ppw != 2))
+    if (t.nimg < 2 || t.nimg > kMaxTrajImgs || a.npts <= 0 || blocks > 0x7fffffffLL || (ppw != 1 && ppw != 2 && ppw != 4))
         return hipErrorInvalidValue;
-    if (ppw == 2) hipLaunchKernelGGL((k_lk<32, true>), dim3((unsigned)blocks), dim3(64), 0, s, a, t);
+    if (ppw == 4) hipLaunchKernelGGL((k_lk<16, true>), dim3((unsigned)blocks), dim3(64), 0, s, a, t);
+    else if (ppw == 2) hipLaunchKernelGGL((k_lk<32, true>), dim3((unsigned)blocks), dim3(64), 0, s, a, t);
     else hipLaunchKernelGGL((k_lk<64, true>), dim3((unsigned)blocks), dim3(64), 0, s, a, t);
     return hipGetLastError();
 }
