@@ -250,6 +250,14 @@ int mdx_flow_trajectory(mdx_ctx* ctx, const uint8_t* const* imgs, int nimg, int 
                         int* num_vectors);
 
 /*
+ * One host block for a trajectory call's outputs.  With traj, start_pts, vectors and traj_len at
+ * these byte offsets of one block (e.g. from mdx_host_alloc), mdx_flow_trajectory and
+ * mdx_ring_trajectory read all four back with one copy instead of four.  offsets[] = {traj,
+ * start_pts, vectors, traj_len}; returns the block size in bytes.  Any other placement works too.
+ */
+size_t mdx_trajectory_layout(int npts, int nimg, size_t offsets[4]);
+
+/*
  * Resident frame ring for the live chain: the node's raw_images_ deque (motion_detection_node.h:82,
  * filled at node.cpp:248-261), whose every frame the reference re-converts, re-uploads and
  * re-pyramids on each callback (:266-287, then optical_flow_calculator.cpp:166-170).  Here a frame

@@ -38,7 +38,7 @@ EXPORTED = [
     "mdx_srand", "mdx_rand", "mdx_fit_subspace", "mdx_device_pci", "mdx_build_info",
     "mdx_ring_push", "mdx_ring_trajectory", "mdx_ring_reset", "mdx_input_ready",
     "mdx_host_alloc", "mdx_host_free", "mdx_probe_stream3_dev", "mdx_lk_fallbacks",
-    "mdx_debug_div32",
+    "mdx_debug_div32", "mdx_trajectory_layout",
 ]
 
 # csrc/Makefile STAMPED: the files whose bytes the library's provenance stamp hashes, in order
@@ -156,6 +156,9 @@ def lib() -> C.CDLL:
     if hasattr(L, "mdx_lk_fallbacks"):
         L.mdx_lk_fallbacks.argtypes = [vp, C.POINTER(C.c_longlong)]
         L.mdx_lk_fallbacks.restype = C.c_int
+    if hasattr(L, "mdx_trajectory_layout"):
+        L.mdx_trajectory_layout.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_size_t)]
+        L.mdx_trajectory_layout.restype = C.c_size_t
     if hasattr(L, "mdx_host_alloc"):
         L.mdx_host_alloc.argtypes = [C.c_size_t]
         L.mdx_host_alloc.restype = vp

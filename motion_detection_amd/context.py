@@ -200,11 +200,24 @@ class Context:
         return out
 
     def trajectory_buffers(self, w: int, h: int, nimg: int, pinned: bool = False) -> "TrajectoryResult":
-        """Output arrays of a trajectory call; pinned=True puts them in page-locked memory."""
+        """Output arrays of a trajectory call; pinned=True puts them in one page-locked block laid
+        out as mdx_trajectory_layout says, so the call reads them back with one copy."""
         n = grid_count(w, h, self.params.pixel_step)
-        mk = (lambda shape, dt: host_empty(shape, dt)) if pinned else (lambda shape, dt: np.zeros(shape, dt))
-        return TrajectoryResult(0, mk((n, nimg, 2), np.float32), mk((n,), np.int32), mk((n, 2), np.float32),
-                                mk((n, 4), np.float64))
+        if not pinned:
+            return TrajectoryResult(0, np.zeros((n, nimg, 2), np.float32), np.zeros((n,), np.int32),
+                                    np.zeros((n, 2), np.float32), np.zeros((n, 4), np.float64))
+        if not hasattr(lib(), "mdx_trajectory_layout"):
+            return TrajectoryResult(0, host_empty((n, nimg, 2), np.float32), host_empty((n,), np.int32),
+                                    host_empty((n, 2), np.float32), host_empty((n, 4), np.float64))
+        off = (C.c_size_t * 4)()
+        total = int(lib().mdx_trajectory_layout(n, nimg, off))
+        blk = host_empty((total,), np.uint8)
+
+        def part(o, shape, dt):
+            cnt = int(np.prod(shape))
+            return blk[o:o + cnt * np.dtype(dt).itemsize].view(dt).reshape(shape)
+        return TrajectoryResult(0, part(off[0], (n, nimg, 2), np.float32), part(off[3], (n,), np.int32),
+                                part(off[1], (n, 2), np.float32), part(off[2], (n, 4), np.float64))
 
     def ring_reset(self) -> None:
         self._check(lib().mdx_ring_reset(self._h))

@@ -56,6 +56,7 @@ struct mdx_ctx {
     // recomputed), read back and cleared at the sync points, accumulated in lk_fallback
     DevBuf errw;
     int* err_host = nullptr;                 // pinned readback
+    int* tcnt_host = nullptr;                // pinned readback of the trajectory counts
     long long lk_fallback[3] = {0, 0, 0};
     int spin_max = kLkSpinDefault;           // MDX_LK_SPIN_MAX (debug: < 0 injects timeouts)
     int lk_cap = 85;                         // MDX_LK_CAP: dataflow launch share of the resident waves (%)
@@ -72,7 +73,7 @@ struct mdx_ctx {
     DevBuf cls, Abuf, ctab;                  // LK v2: class planes, A sums, residue tables
     DevBuf dbg;                              // LK v2 per-level trace (MDX_LK_DEBUG=1)
     DevBuf csum;                             // classify: per-block summaries
-    DevBuf tin, tcur, tnp, tst, ttraj, tlen, tvec, tstart, tnum, tflag;   // trajectory tracking
+    DevBuf tin, tcur, tnp, tst, ttraj, tnum, tflag;   // trajectory tracking (ttraj: the four outputs, one block)
     DevBuf straj, sdata, sq, scnt, scols, sres, sout, sbest;      // subspace RANSAC
     DevBuf ring_pyr, ring_der, rin;          // resident frame ring (mdx_ring_*)
     DevBuf wscr;                             // k_warp_prep's per-pair / per-tile tables
@@ -482,12 +483,13 @@ extern "C" int mdx_destroy(mdx_ctx* c)
     DevBuf* bufs[] = {&c->pyr1, &c->pyr2, &c->der, &c->fits, &c->in1, &c->in2, &c->np, &c->st,
                       &c->vec, &c->mask, &c->H, &c->Hext, &c->num, &c->bnp, &c->bst,
                       &c->cls, &c->Abuf, &c->ctab, &c->dbg, &c->csum, &c->tin, &c->tcur, &c->tnp, &c->tst,
-                      &c->ttraj, &c->tlen, &c->tvec, &c->tstart, &c->tnum, &c->tflag, &c->straj, &c->sdata, &c->sq,
+                      &c->ttraj, &c->tnum, &c->tflag, &c->straj, &c->sdata, &c->sq,
                       &c->scnt, &c->scols, &c->sres, &c->sout, &c->sbest, &c->ring_pyr, &c->ring_der, &c->rin,
                       &c->errw, &c->wscr, &c->rsc};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (c->err_host) (void)hipHostFree(c->err_host);
+    if (c->tcnt_host) (void)hipHostFree(c->tcnt_host);
     if (c->ev) {
         for (int i = 0; i < mdx_ctx::kSlots * 7; i++) (void)hipEventDestroy(c->ev[i]);
         delete[] c->ev;
@@ -1015,6 +1017,20 @@ extern "C" int mdx_flow_warp_diff(mdx_ctx* c, const uint8_t* img1, const uint8_t
 // points the previous pass left from frame j (pyr[j], der[j]) to frame j + 1 (pyr[j + 1]).  Every
 // pass runs the point LK from the carried points: for one pair it is faster than the class-plane
 // kernels even on the grid start points of pass 0, whose per-level tails one pair cannot fill.
+extern "C" size_t mdx_trajectory_layout(int npts, int nimg, size_t offsets[4])
+{
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t p = (size_t)(npts > 0 ? npts : 1), n = (size_t)(nimg > 0 ? nimg : 1);
+    size_t o[4];
+    o[0] = 0;
+    o[1] = al(p * n * 8);
+    o[2] = o[1] + al(p * 8);
+    o[3] = o[2] + al(p * 32);
+    if (offsets)
+        for (int i = 0; i < 4; i++) offsets[i] = o[i];
+    return o[3] + p * 4;
+}
+
 static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int h, const uint8_t* const* pyr,
                              const uint32_t* const* der, float* traj, int32_t* traj_len, float* start_pts,
                              double* vectors, int* num_vectors)
@@ -1027,15 +1043,23 @@ static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int
     if ((rc = ensure(c, c->tcur, pts * 8)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->tnp, pts * 8)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->tst, pts)) != MDX_OK) return rc;
-    if ((rc = ensure(c, c->ttraj, pts * nimg * 8)) != MDX_OK) return rc;
-    if ((rc = ensure(c, c->tlen, pts * 4)) != MDX_OK) return rc;
-    if ((rc = ensure(c, c->tvec, pts * 32)) != MDX_OK) return rc;
-    if ((rc = ensure(c, c->tstart, pts * 8)) != MDX_OK) return rc;
+    // the four outputs in one block, laid out as mdx_trajectory_layout says (one readback copy
+    // when the host block matches)
+    size_t off[4];
+    const size_t obytes = mdx_trajectory_layout(npts, nimg, off);
+    if ((rc = ensure(c, c->ttraj, obytes)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->tnum, 8)) != MDX_OK) return rc;
+    if (!c->tcnt_host && hipHostMalloc((void**)&c->tcnt_host, 16, hipHostMallocDefault) != hipSuccess) {
+        c->tcnt_host = nullptr;
+        return set_err(c, MDX_ENOMEM, "trajectory passes: hipHostMalloc(counts)");
+    }
     hipStream_t s = c->stream;
     float* cur = c->tcur.as<float>();
-    float* tr = c->ttraj.as<float>();
-    int* tl = c->tlen.as<int>();
+    uint8_t* ob = c->ttraj.as<uint8_t>();
+    float* tr = reinterpret_cast<float*>(ob + off[0]);
+    float* tstart = reinterpret_cast<float*>(ob + off[1]);
+    double* tvec = reinterpret_cast<double*>(ob + off[2]);
+    int* tl = reinterpret_cast<int*>(ob + off[3]);
     int* dnum = c->tnum.as<int>();
     const bool chain = c->traj_chain && nimg <= kMaxTrajImgs && npts > 0;
     if (chain && (rc = ensure(c, c->tflag, pts * 4)) != MDX_OK) return rc;
@@ -1067,8 +1091,8 @@ static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int
         t.traj = tr;
         t.tlen = tl;
         t.flag = c->tflag.as<int>();
-        t.vectors = c->tvec.as<double>();
-        t.start_pts = c->tstart.as<float>();
+        t.vectors = tvec;
+        t.start_pts = tstart;
         t.num = dnum;
         t.mvs = P.min_vector_size;
         HIP_OR_RETURN(c, launch_lk_chain(s, a, t, c->traj_ppw));
@@ -1093,22 +1117,30 @@ static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int
         a.prev_pts = cur;
         if ((rc = run_lk(c, g, a, 1, w, h, 0, ny, true)) != MDX_OK) return rc;
         HIP_OR_RETURN(c, launch_traj_update(s, npts, c->tnp.as<float>(), c->tst.as<uint8_t>(), cur, tr, tl, nimg, w, h,
-                                            j == nimg - 2, P.min_vector_size, c->tvec.as<double>(),
-                                            c->tstart.as<float>(), dnum));
+                                            j == nimg - 2, P.min_vector_size, tvec, tstart, dnum));
     }
     int num = 0;
     if (npts > 0) {
-        if (traj) HIP_OR_RETURN(c, hipMemcpyAsync(traj, tr, (size_t)npts * nimg * 8, hipMemcpyDeviceToHost, s));
-        if (traj_len) HIP_OR_RETURN(c, hipMemcpyAsync(traj_len, tl, (size_t)npts * 4, hipMemcpyDeviceToHost, s));
-        if (start_pts) HIP_OR_RETURN(c, hipMemcpyAsync(start_pts, c->tstart.p, (size_t)npts * 8, hipMemcpyDeviceToHost, s));
-        if (vectors) HIP_OR_RETURN(c, hipMemcpyAsync(vectors, c->tvec.p, (size_t)npts * 32, hipMemcpyDeviceToHost, s));
+        uint8_t* hb = reinterpret_cast<uint8_t*>(traj);
+        const bool one_block = traj && start_pts && vectors && traj_len &&
+                               reinterpret_cast<uint8_t*>(start_pts) == hb + off[1] &&
+                               reinterpret_cast<uint8_t*>(vectors) == hb + off[2] &&
+                               reinterpret_cast<uint8_t*>(traj_len) == hb + off[3];
+        if (one_block) {
+            HIP_OR_RETURN(c, hipMemcpyAsync(hb, ob, off[3] + (size_t)npts * 4, hipMemcpyDeviceToHost, s));
+        } else {
+            if (traj) HIP_OR_RETURN(c, hipMemcpyAsync(traj, tr, (size_t)npts * nimg * 8, hipMemcpyDeviceToHost, s));
+            if (traj_len) HIP_OR_RETURN(c, hipMemcpyAsync(traj_len, tl, (size_t)npts * 4, hipMemcpyDeviceToHost, s));
+            if (start_pts) HIP_OR_RETURN(c, hipMemcpyAsync(start_pts, tstart, (size_t)npts * 8, hipMemcpyDeviceToHost, s));
+            if (vectors) HIP_OR_RETURN(c, hipMemcpyAsync(vectors, tvec, (size_t)npts * 32, hipMemcpyDeviceToHost, s));
+        }
     }
-    int counts[2] = {0, 0};
-    HIP_OR_RETURN(c, hipMemcpyAsync(counts, dnum, chain ? 8 : 4, hipMemcpyDeviceToHost, s));
+    c->tcnt_host[0] = c->tcnt_host[1] = 0;
+    HIP_OR_RETURN(c, hipMemcpyAsync(c->tcnt_host, dnum, chain ? 8 : 4, hipMemcpyDeviceToHost, s));
     HIP_OR_RETURN(c, hipStreamSynchronize(s));
-    num = counts[0];
-    if (chain && counts[1] != 0)
-        return set_err(c, MDX_EHIP, "trajectory passes: %d point hand-off(s) timed out", counts[1]);
+    num = c->tcnt_host[0];
+    if (chain && c->tcnt_host[1] != 0)
+        return set_err(c, MDX_EHIP, "trajectory passes: %d point hand-off(s) timed out", c->tcnt_host[1]);
     if (num_vectors) *num_vectors = num;
     return MDX_OK;
 }
