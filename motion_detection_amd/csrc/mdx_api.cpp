@@ -1184,7 +1184,7 @@ extern "C" int mdx_flow_trajectory(mdx_ctx* c, const uint8_t* const* imgs, int n
     uint32_t* der = c->der.as<uint32_t>();
     HIP_OR_RETURN(c, launch_front(s, npairs, din, din + fbytes, w, h, stride, (long long)fbytes, fmt, pyr1, pyr2, g));
     HIP_OR_RETURN(c, launch_pyr_levels(s, npairs, pyr1, pyr2, g));
-    for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, npairs, pyr1, der, g, l));
+    HIP_OR_RETURN(c, launch_scharr_levels(s, npairs, pyr1, der, g));
     // frame j's pyramid is slot j of pyr1 (j < nimg-1) and the last frame's slot nimg-2 of pyr2
     std::vector<const uint8_t*> fp(nimg);
     std::vector<const uint32_t*> fd(nimg);
@@ -1283,7 +1283,7 @@ extern "C" int mdx_ring_push(mdx_ctx* c, const uint8_t* img, int w, int h, int s
     HIP_OR_RETURN(c, launch_front(s, 1, c->rin.as<uint8_t>(), c->rin.as<uint8_t>(), w, h, stride, (long long)fbytes, fmt,
                                   pyr, pyr, g, 1));
     HIP_OR_RETURN(c, launch_pyr_levels(s, 1, pyr, pyr, g, 1));
-    for (int l = 0; l < g.nlev; l++) HIP_OR_RETURN(c, launch_scharr(s, 1, pyr, der, g, l));
+    HIP_OR_RETURN(c, launch_scharr_levels(s, 1, pyr, der, g));
     c->ring_order.push_back(slot);
     while ((int)c->ring_order.size() > keep) c->ring_order.erase(c->ring_order.begin());
     return (int)c->ring_order.size();

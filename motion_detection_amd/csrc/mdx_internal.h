@@ -179,6 +179,8 @@ hipError_t launch_front(hipStream_t s, int batch, const uint8_t* in1, const uint
 hipError_t launch_pyr_levels(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* pyr2, const Geometry& g, int fsel = 0,
                              const RowSpan* rows = nullptr);
 // padded rows [prow0, prow1) of the level's derivative planes (default: all)
+// every level's Scharr planes, whole levels, one launch
+hipError_t launch_scharr_levels(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g);
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level,
                          int prow0 = 0, int prow1 = -1);
 hipError_t launch_lk(hipStream_t s, int batch, const LkArgs& a);

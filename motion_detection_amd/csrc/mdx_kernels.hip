@@ -1624,7 +1624,11 @@ static hipError_t launch_front_bands(hipStream_t s, FrontArgs& a, int mode, int 
     // else 1; beyond 64 KB (rows wider than ~8.7K px at RB = 1) the launch asks for the larger
     // dynamic LDS explicitly (up to the CU's 160 KB)
     auto lds_of = [&](int rb) { return (size_t)(2 * rb + 3) * a.lp + (size_t)rb * a.lp1; };
-    const int rb = lds_of(4) <= 32 * 1024 ? 4 : lds_of(2) <= 64 * 1024 ? 2 : 1;
+    int rb = lds_of(4) <= 32 * 1024 ? 4 : lds_of(2) <= 64 * 1024 ? 2 : 1;
+    // a single frame (the live ring's push): 4-row bands are a few hundred workgroups, under two
+    // per CU; one-row bands re-read more source rows (5 per destination row against 2.75) but
+    // spread the frame over the chip
+    if (rb == 4 && (long long)a.nz * ((a.L1.h + 3) / 4) < 512) rb = 1;
     const size_t lds = lds_of(rb);
     // k_front's static arrays (out0, out1, nout) share the CU's 160 KB with the dynamic rows
     const size_t lds_static = (size_t)(2 * rb + 80 + rb + 80 + 2) * sizeof(int);
@@ -1699,6 +1703,74 @@ hipError_t launch_pyr_levels(hipStream_t s, int batch, uint8_t* pyr1, uint8_t* p
         if (hipError_t e = launch_front_bands(s, a, 2, rows ? rows[l].lo : 0, rows ? rows[l].hi : -1)) return e;
     }
     return hipSuccess;
+}
+
+// Every level's Scharr planes in one launch (blockIdx.y runs over the levels' padded rows, level by
+// level): the live ring's push builds one frame's five levels, whose launches are each a few
+// microseconds of mostly launch overhead.
+struct ScharrLevels {
+    Level L[kMaxLevels];
+    int nchunk[kMaxLevels];
+    int row0[kMaxLevels + 1];   // first blockIdx.y of each level
+    int nlev;
+};
+__global__ __launch_bounds__(256) void k_scharr_levels(const uint8_t* __restrict__ pyr1, uint32_t* __restrict__ der,
+                                                       long long img_bytes, long long der_words, ScharrLevels sl)
+{
+    int l = 0;
+    while (l + 1 < sl.nlev && (int)blockIdx.y >= sl.row0[l + 1]) l++;
+    const Level L = sl.L[l];
+    const int nchunk = sl.nchunk[l];
+    const int pair = blockIdx.z;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x + 4;         // word chunks 0..3 are margin
+    const int py = (int)blockIdx.y - sl.row0[l] - kPad;
+    if (c > nchunk) return;
+    const int px0 = 4 * c - kXOff;
+    uint32_t o[4] = {0, 0, 0, 0};
+    if (py >= 0 && py < L.h && px0 + 4 > 0 && px0 < L.w) {
+        const uint8_t* s = pyr1 + (long long)pair * img_bytes + L.img_off + L.core() + (long long)py * L.pitch + px0 - 4;
+        const int p = L.pitch;
+        uint32_t rw[3][3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const u3a4k v = *reinterpret_cast<const u3a4k*>(s + (long long)(r - 1) * p);
+            rw[r][0] = v.x; rw[r][1] = v.y; rw[r][2] = v.z;
+        }
+        auto B = [&](int r, int b) -> int { return (int)((rw[r][b >> 2] >> (8 * (b & 3))) & 255u); };
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int px = px0 + i;
+            if (px < 0 || px >= L.w) continue;
+            const int bm = 3 + i, bc = 4 + i, bp = 5 + i;               // bytes x-1, x, x+1
+            const int t0m = (B(0, bm) + B(2, bm)) * 3 + B(1, bm) * 10;
+            const int t0p = (B(0, bp) + B(2, bp)) * 3 + B(1, bp) * 10;
+            const int t1m = B(2, bm) - B(0, bm), t1c = B(2, bc) - B(0, bc), t1p = B(2, bp) - B(0, bp);
+            const int ix = t0p - t0m;
+            const int iy = (t1m + t1p) * 3 + t1c * 10;
+            o[i] = (uint32_t)(uint16_t)(int16_t)ix | ((uint32_t)(uint16_t)(int16_t)iy << 16);
+        }
+    }
+    uint32_t* row = der + (long long)pair * der_words + L.der_off + (long long)(py + kPad) * L.pitch;
+    *reinterpret_cast<uint4*>(row + 4 * c) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+hipError_t launch_scharr_levels(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g)
+{
+    ScharrLevels sl{};
+    sl.nlev = g.nlev;
+    int rows = 0, maxc = 0;
+    for (int l = 0; l < g.nlev; l++) {
+        sl.L[l] = g.lv[l];
+        sl.nchunk[l] = (kXOff + g.lv[l].w + kPad - 1) / 4;
+        sl.row0[l] = rows;
+        rows += g.lv[l].rows;
+        maxc = std::max(maxc, sl.nchunk[l]);
+    }
+    sl.row0[g.nlev] = rows;
+    if (rows == 0) return hipSuccess;
+    const dim3 grid((maxc - 4 + 1 + 63) / 64, rows, batch);
+    hipLaunchKernelGGL(k_scharr_levels, grid, dim3(64), 0, s, pyr1, der, g.img_bytes, g.der_words, sl);
+    return hipGetLastError();
 }
 
 hipError_t launch_scharr(hipStream_t s, int batch, const uint8_t* pyr1, uint32_t* der, const Geometry& g, int level,
