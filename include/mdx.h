@@ -254,6 +254,9 @@ int mdx_flow_trajectory(mdx_ctx* ctx, const uint8_t* const* imgs, int nimg, int 
  * these byte offsets of one block (e.g. from mdx_host_alloc), mdx_flow_trajectory and
  * mdx_ring_trajectory read all four back with one copy instead of four.  offsets[] = {traj,
  * start_pts, vectors, traj_len}; returns the block size in bytes.  Any other placement works too.
+ * Outputs that are all in page-locked memory (mdx_host_alloc) are written by the chained launch
+ * itself through their device mapping, with no readback copy.  Either way traj's entries past
+ * traj_len[i] are 0.
  */
 size_t mdx_trajectory_layout(int npts, int nimg, size_t offsets[4]);
 

@@ -1062,6 +1062,7 @@ static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int
     int* tl = reinterpret_cast<int*>(ob + off[3]);
     int* dnum = c->tnum.as<int>();
     const bool chain = c->traj_chain && nimg <= kMaxTrajImgs && npts > 0;
+    bool direct = false;   // the chained launch writes the caller's mapped outputs itself
     if (chain && (rc = ensure(c, c->tflag, pts * 4)) != MDX_OK) return rc;
     HIP_OR_RETURN(c, launch_traj_init(s, npts, ny, P.pixel_step, nimg, cur, tr, tl, dnum,
                                       chain ? c->tflag.as<int>() : nullptr));
@@ -1093,6 +1094,25 @@ static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int
         t.flag = c->tflag.as<int>();
         t.vectors = tvec;
         t.start_pts = tstart;
+        // the caller's outputs in mapped page-locked memory (mdx_host_alloc): the launch writes them
+        if (npts > 0 && traj && traj_len && start_pts && vectors) {
+            auto mapped = [](void* p) -> void* {
+                hipPointerAttribute_t at{};
+                if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+                    (void)hipGetLastError();   // pageable memory: not an error here
+                    return nullptr;
+                }
+                return at.type == hipMemoryTypeHost ? at.devicePointer : nullptr;
+            };
+            void* m[4] = {mapped(traj), mapped(traj_len), mapped(start_pts), mapped(vectors)};
+            if (m[0] && m[1] && m[2] && m[3]) {
+                t.htraj = static_cast<float*>(m[0]);
+                t.htlen = static_cast<int*>(m[1]);
+                t.hstart = static_cast<float*>(m[2]);
+                t.hvec = static_cast<double*>(m[3]);
+                direct = true;
+            }
+        }
         t.num = dnum;
         t.mvs = P.min_vector_size;
         HIP_OR_RETURN(c, launch_lk_chain(s, a, t, c->traj_ppw));
@@ -1120,7 +1140,7 @@ static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int
                                             j == nimg - 2, P.min_vector_size, tvec, tstart, dnum));
     }
     int num = 0;
-    if (npts > 0) {
+    if (npts > 0 && !direct) {
         uint8_t* hb = reinterpret_cast<uint8_t*>(traj);
         const bool one_block = traj && start_pts && vectors && traj_len &&
                                reinterpret_cast<uint8_t*>(start_pts) == hb + off[1] &&

@@ -201,6 +201,12 @@ struct TrajChain {
     float* start_pts;                    // [npts][2] start points of the last pass, or null
     int* num;                            // [0] num_vectors, [1] hand-off waits that timed out
     double mvs;                          // min_vector_size
+    // the caller's page-locked outputs, device-mapped (or null): the passes write traj, traj_len,
+    // start_pts and vectors straight into them, and no readback copy follows
+    float* htraj;
+    int* htlen;
+    float* hstart;
+    double* hvec;
 };
 // ppw: points per wave (1: 64 lanes per point, 2: 32, 4: 16)
 hipError_t launch_lk_chain(hipStream_t s, const LkArgs& a, const TrajChain& t, int ppw);

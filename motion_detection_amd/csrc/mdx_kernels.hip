@@ -897,10 +897,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
         // k_traj_update's bookkeeping for this point and pass (optical_flow_calculator.cpp:178-242)
         if (valid && s == 0) {
             const bool last = pass == t.nimg - 2;
-            double* v = (last && t.vectors) ? t.vectors + 4LL * pt : nullptr;
-            if (last && t.start_pts) {
-                t.start_pts[2 * pt] = px0;
-                t.start_pts[2 * pt + 1] = py0;
+            // outputs: the caller's mapped page-locked arrays when given, else the device ones
+            float* tj = t.htraj ? t.htraj : t.traj;
+            double* vv = t.hvec ? t.hvec : t.vectors;
+            float* sp0 = t.hstart ? t.hstart : t.start_pts;
+            double* v = (last && vv) ? vv + 4LL * pt : nullptr;
+            if (t.htraj && pass == 0) {   // k_traj_init wrote the device row's start
+                tj[(long long)pt * t.nimg * 2] = px0;
+                tj[(long long)pt * t.nimg * 2 + 1] = py0;
+            }
+            if (last && sp0) {
+                sp0[2 * pt] = px0;
+                sp0[2 * pt + 1] = py0;
             }
             if (status) {
                 const float ex = npx, ey = npy;
@@ -918,12 +926,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
                                        __builtin_bit_cast(unsigned long long, make_float2(ex, ey)), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                     const int l = __hip_atomic_load(t.tlen + pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    t.traj[((long long)pt * t.nimg + l) * 2] = ex;
-                    t.traj[((long long)pt * t.nimg + l) * 2 + 1] = ey;
+                    tj[((long long)pt * t.nimg + l) * 2] = ex;
+                    tj[((long long)pt * t.nimg + l) * 2 + 1] = ey;
                     __hip_atomic_store(t.tlen + pt, l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             } else if (v) {
                 v[0] = -1.0; v[1] = -1.0; v[2] = 0.0; v[3] = 0.0;
+            }
+            if (last && t.htraj) {
+                // the mapped row's entries past traj_len (the device rows were zeroed by k_traj_init;
+                // every entry of a mapped row is written once) and traj_len itself
+                const int lf = __hip_atomic_load(t.tlen + pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (int k = lf; k < t.nimg; k++) {
+                    tj[((long long)pt * t.nimg + k) * 2] = 0.f;
+                    tj[((long long)pt * t.nimg + k) * 2 + 1] = 0.f;
+                }
+                t.htlen[pt] = lf;
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(t.flag + pt, pass + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1805,6 +1823,7 @@ __global__ void k_traj_init(int npts, int ny, int pixel_step, int nimg, float* _
     cur[2 * i + 1] = y;
     traj[(long long)i * nimg * 2] = x;
     traj[(long long)i * nimg * 2 + 1] = y;
+    for (int k = 2; k < 2 * nimg; k++) traj[(long long)i * nimg * 2 + k] = 0.f;   // entries past traj_len: 0
     tlen[i] = 1;
 }
 

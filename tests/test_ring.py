@@ -117,3 +117,25 @@ def test_pinned_views_keep_the_block_alive(mdx):
     for i, v in enumerate(views):
         v[...] = i + 1                                    # use after free if the block was released
         assert int(v.sum()) == (i + 1) * 64 * 64
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nimg", [5, 3])
+def test_mapped_outputs_equal_copied_outputs(mdx, ctx, oracle, nimg):
+    """Outputs in one page-locked block (trajectory_buffers(pinned=True), mdx_trajectory_layout) are
+    written by the chained launch itself; pageable ones are copied back.  Both hold the same bits,
+    entries past traj_len included (0), and match the oracle."""
+    w, h = 320, 240
+    frames = sequence(mdx, oracle, w, h, nimg, seed=77, channels=3)
+    ctx.ring_reset()
+    for f in frames:
+        ctx.ring_push(f, nimg)
+    mapped = ctx.ring_trajectory(w, h, nimg, out=ctx.trajectory_buffers(w, h, nimg, pinned=True))
+    copied = ctx.ring_trajectory(w, h, nimg, out=ctx.trajectory_buffers(w, h, nimg, pinned=False))
+    assert mapped.num_vectors == copied.num_vectors
+    for a, b in [(mapped.traj, copied.traj), (mapped.traj_len, copied.traj_len), (mapped.start_pts, copied.start_pts),
+                 (mapped.vectors, copied.vectors)]:
+        assert a.tobytes() == b.tobytes()
+    for i in range(len(mapped.traj_len)):
+        assert not mapped.traj[i, int(mapped.traj_len[i]):].any()
+    _compare(mapped, oracle.flow_trajectory(frames, pixel_step=10, nthreads=8), "mapped")
