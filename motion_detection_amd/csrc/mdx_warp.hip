@@ -575,6 +575,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     }
     const int pair = bid / (nbx * nby), tile = bid - pair * (nbx * nby);
     const int tx_ = tile % nbx, ty_ = tile / nbx;
+    // The tile's scalar operands (the pair's fit, the tile's TileInfo) in ONE round trip: left to
+    // itself the compiler sinks each scalar load into the branch that first uses it, and the DMA
+    // then waits behind five dependent scalar-load latencies (kernel arguments, fit status, more
+    // arguments, M and TileInfo, TileInfo.wd).  The TileInfo of a pair with no fit is not written
+    // by k_warp_prep; it is read (in bounds) and unused.
+    const PairFit& f = fits[pair];
+    const TileInfo t = tinfo[(long long)pair * (nbx * nby) + tile];   // uniform: scalar loads
+    double M[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) M[k] = f.Hinv[k];
+    const int fit_status = f.fit_status;
+    asm volatile("" ::"s"(fit_status), "s"(t.wd), "s"(t.fast), "s"(t.sxa), "s"(t.sya), "s"(t.sw), "s"(t.sh),
+                 "s"(M[0]), "s"(M[1]), "s"(M[2]), "s"(M[3]), "s"(M[4]), "s"(M[5]), "s"(M[6]), "s"(M[7]),
+                 "s"(M[8]), "s"(g1), "s"(g2), "s"(mask), "s"(prep));
     // wave index in an SGPR: the staging loop's trip count and LDS addresses stay scalar
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int x0 = tx_ * kTW, y0 = row0 + ty_ * kTH;
@@ -584,8 +598,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     const uint8_t* g2p = g2 + (long long)pair * g2_stride;
     uint8_t* mp = mask + (long long)pair * mask_stride - (long long)row0 * w;   // indexed by frame row
 
-    const PairFit& f = fits[pair];
-    if (f.fit_status != 0) {   // no fit: the reference produces no mask; ours is all zero
+    if (fit_status != 0) {   // no fit: the reference produces no mask; ours is all zero
         const int nx = max(0, min(4, w - xs));
         for (int r = r0; r < kTH && y0 + r < row1; r += 8) {
             uint8_t* m = mp + (long long)(y0 + r) * w + xs;
@@ -593,14 +606,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         }
         return;
     }
-    double M[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) M[k] = f.Hinv[k];
     const uint8_t* src = g1 + (long long)pair * g1_stride;
     const bool affine = (M[6] == 0.0) && (M[7] == 0.0);
     // fast path only over dword-aligned rows with reference blocks of 64 (uniform per workgroup)
     const bool try_fast = bw0 == kBW && vec_ok;
-    const TileInfo t = tinfo[(long long)pair * (nbx * nby) + tile];   // uniform: scalar loads
     if (!try_fast || !t.fast) {
         // ---- general path: per pixel, global gathers
         const int nx = max(0, min(4, w - xs));
