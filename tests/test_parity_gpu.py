@@ -201,6 +201,37 @@ def test_batch_dev_matches_host_path(mdx, oracle, monkeypatch, B, env, wh):
         np.testing.assert_array_equal(out["H"][i], ref["H"])
 
 
+@pytest.mark.parametrize("w,h", [(320, 240), (640, 480)])
+def test_batch_with_unfit_pair(mdx, oracle, w, h):
+    """A pair with no fit (flat frames) between fitted pairs of one batch: its mask is written all
+    zero (over a garbage-filled buffer) and the neighbours match the oracle.  k_warp_diff reads
+    every tile's TileInfo before testing the pair's fit status; an unfit pair's entries are never
+    written by k_warp_prep, and must stay unused."""
+    B = 3
+    pairs = [mdx.synth_pair(700 + i, w, h, 1) for i in range(B)]
+    flat = np.full((h, w), 77, np.uint8)
+    g1 = np.stack([pairs[0][0], flat, pairs[2][0]]); g2 = np.stack([pairs[0][1], flat.copy(), pairs[2][1]])
+    n = mdx.grid_count(w, h, 10)
+    with mdx.Context(0, w, h, B) as c:
+        c.set_params(pixel_step=10)
+        bufs = {k: c.dev_alloc(s) for k, s in dict(i1=g1.nbytes, i2=g2.nbytes, np=B * n * 8, st=B * n,
+                                                    vec=B * n * 32, mask=B * w * h, H=B * 72, num=B * 4).items()}
+        c.h2d(bufs["i1"], g1); c.h2d(bufs["i2"], g2)
+        c.h2d(bufs["mask"], np.full((B, h, w), 0xAB, np.uint8))
+        c.flow_warp_diff_batch_dev(B, bufs["i1"], bufs["i2"], w, h, w, w * h, mdx.FMT_GRAY8, bufs["np"], bufs["st"],
+                                   bufs["vec"], bufs["mask"], bufs["H"], 0, bufs["num"])
+        c.sync()
+        mask = np.empty((B, h, w), np.uint8); num = np.empty(B, np.int32)
+        c.d2h(mask, bufs["mask"]); c.d2h(num, bufs["num"])
+        for p in bufs.values():
+            c.dev_free(p)
+    assert num[1] == 0 and mask[1].max() == 0
+    for i in (0, 2):
+        ref = oracle.calculate_optical_flow(g1[i], g2[i], pixel_step=10)
+        assert num[i] == ref["num_vectors"] >= 4
+        np.testing.assert_array_equal(mask[i], ref["mask"])
+
+
 def test_reference_interface(mdx, oracle):
     """OpticalFlowCalculator.calculateOpticalFlow fills the vector Mat and comp like the reference."""
     a, b, _ = mdx.synth_pair(8, 320, 240, 3)
