@@ -536,6 +536,9 @@ def main():
     ap.add_argument("--roofline-config", default="4k", choices=sorted(CONFIGS))
     ap.add_argument("--roofline-batch", type=int, default=32)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--roofline-warmup", type=int, default=200,
+                    help="untimed launches before each roofline leg's timed ones: after idle, a burst of warp "
+                         "launches runs its first ~120 in a clock / power transient (profiles/r05_warp_transient.txt)")
     ap.add_argument("--roofline-h", default="both", choices=["both", "affine", "projective"],
                     help="roofline leg launches: the affine true H, the projective H, or both (profiling passes "
                          "take one kind at a time so per-launch counters and records stay per kind)")
@@ -752,8 +755,12 @@ def main():
         eH, eM = rctx.dev_alloc(Hb.nbytes), rctx.dev_alloc(RB * rw * rh)
         rctx.h2d(e1, r1); rctx.h2d(e2, r2); rctx.h2d(eH, Hb)
         launch_ms = None
+        # warmup: a burst of launches after idle runs in a clock / power transient (k_warp_diff 157 ->
+        # 180-190 -> 141 us over its first ~120 launches on the same inputs, the copy probe flat at
+        # 121 us: profiles/r05_warp_transient.txt), so each leg is timed after roofline_warmup launches
+        rwarm = max(2, args.warmup, args.roofline_warmup)
         if args.roofline_h != "projective":
-            for _ in range(max(2, args.warmup)):
+            for _ in range(rwarm):
                 rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
             rctx.device_sync()
             rctx.enable_timing(True)
@@ -766,7 +773,7 @@ def main():
         achieved = alg_bytes / (launch_ms * 1e-3) / 1e9 if launch_ms else None
         # the memory ceiling of this access mix: the same 3 B/px as one linear non-temporal pass
         # (mdx_probe_stream3_dev, same buffers, same event bracketing)
-        for _ in range(2):
+        for _ in range(rwarm):
             rctx.probe_stream3_dev(RB * rw * rh, e1, e2, eM)
         rctx.device_sync()
         rctx.enable_timing(True)
@@ -783,7 +790,7 @@ def main():
         projective = None
         if args.roofline_h != "affine":
             rctx.h2d(eH, np.ascontiguousarray(np.broadcast_to(Hp, (RB, 3, 3)), dtype=np.float64))
-            for _ in range(2):
+            for _ in range(rwarm):
                 rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
             rctx.device_sync()
             rctx.enable_timing(True)
@@ -811,6 +818,7 @@ def main():
                     frac=round(achieved / HBM_PEAK_GBS, 4) if achieved else None, traffic=traffic, kernel="k_warp_diff",
                     workload=f"{rw}x{rh} gray, {RB} pairs per launch, true H (affine), 3 B/px algorithmic",
                     avg_launch_us=round(launch_ms * 1e3, 2) if launch_ms else None,
+                    timed_launches=args.steps, warmup_launches=rwarm,
                     algorithmic_bytes_per_launch=int(alg_bytes),
                     copy_ceiling=dict(achieved=round(copy_gbs, 1), avg_launch_us=round(copy_ms * 1e3, 2),
                                       what="linear 3 B/px pass, 16 B/lane, non-temporal (k_stream3)"),

@@ -3,7 +3,9 @@ the average kernel-record duration of the roofline leg's launches (k_warp_prep +
 the copy-ceiling probe (k_stream3), and the fractions of the 8 TB/s peak they give for the 3 B/px
 algorithmic bytes.
 bench.py attaches it as roofline.kernel_trace when its src_sha256 matches the loaded library.
-Usage: python scripts/kt_warp_to_json.py gpurun_out/r04/warp_kt 3840x2160x32 [out.json]
+Usage: python scripts/kt_warp_to_json.py gpurun_out/r04/warp_kt 3840x2160x32 [out.json] [timed]
+timed: average only the last `timed` launches of each kernel (the leg's timed launches; the ones
+before are its warmup, bench.py --roofline-warmup).
 """
 import csv
 import glob
@@ -27,7 +29,8 @@ def bench_stamp(d):
 
 
 d, config = sys.argv[1], sys.argv[2]
-out = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(__file__), "..", "profiles",
+timed = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+out = sys.argv[3] if len(sys.argv) > 3 and sys.argv[3] != "-" else os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                          "warp_kernel_trace.json")
 w, h, b = (int(v) for v in config.split("x"))
 alg = 3.0 * w * h * b
@@ -41,9 +44,13 @@ for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
             # the roofline launches are the large grids (k_warp_diff: w*h*b/32 threads; k_stream3: /16)
             big = threads >= prep_threads if k == "k_warp_prep" else threads >= (w * h * b) // 64
             if k in name and big:
-                dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                dur[k].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+for k in dur:
+    dur[k] = [x for _, x in sorted(dur[k])]
+    if timed:
+        dur[k] = dur[k][-timed:]
 res = dict(config=config, algorithmic_bytes_per_launch=int(alg), source=os.path.basename(os.path.normpath(d)),
-           src_sha256=bench_stamp(d))
+           src_sha256=bench_stamp(d), averaged=f"last {timed} launches per kernel" if timed else "all launches")
 for k, v in dur.items():
     if not v:
         continue

@@ -4,7 +4,7 @@
 # Usage: bash scripts/pmc_warp.sh [out dir, default gpurun_out/pmc_warpc]
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 out=${1:-gpurun_out/pmc_warpc}; mkdir -p $out
-ARGS="--only-roofline --roofline-h affine --steps 3 --warmup 1 --no-cpu"
+ARGS="--only-roofline --roofline-h affine --steps 3 --warmup 1 --roofline-warmup 2 --no-cpu"
 S1="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
 S2="SQ_INSTS_SALU SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
 i=0

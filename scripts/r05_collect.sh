@@ -10,7 +10,7 @@ out=gpurun_out/r05; mkdir -p $out
 export TMPDIR=/tmp
 step() { echo "== $1 $(date +%T)"; }
 if [ "$part" = w ]; then   # the warp evidence alone (also in part b)
-    BENCH_ARGS="--only-roofline --roofline-h affine --steps 3 --warmup 1 --no-cpu" \
+    BENCH_ARGS="--only-roofline --roofline-h affine --steps 3 --warmup 1 --roofline-warmup 2 --no-cpu" \
         bash scripts/pmc_sets.sh warp "FETCH_SIZE" "WRITE_SIZE" > $out/pmc_warp.log 2>&1 || exit 1
     mkdir -p $out/warp_kt $out/warp_kt_proj
     timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $out/warp_kt -o run --output-format csv -- python3 bench.py \
@@ -37,7 +37,7 @@ else
     BENCH_ARGS="--steps 2 --warmup 1 --no-cpu --no-roofline --no-live --no-4k --no-ransac --no-lk-roofline" \
         bash scripts/pmc_sets.sh step "FETCH_SIZE" "WRITE_SIZE" > $out/pmc_step.log 2>&1 || exit 1
     step pmc_warp
-    BENCH_ARGS="--only-roofline --roofline-h affine --steps 3 --warmup 1 --no-cpu" \
+    BENCH_ARGS="--only-roofline --roofline-h affine --steps 3 --warmup 1 --roofline-warmup 2 --no-cpu" \
         bash scripts/pmc_sets.sh warp "FETCH_SIZE" "WRITE_SIZE" > $out/pmc_warp.log 2>&1 || exit 1
     step pmc_warp_counters
     bash scripts/pmc_warp.sh gpurun_out/pmc_warpc > $out/pmc_warpc.log 2>&1 || exit 1
