@@ -13,6 +13,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <cmath>
 
@@ -226,6 +228,20 @@ static int ensure_workspace(mdx_ctx* c, const Geometry& g, int batch, bool two)
     if ((rc = ensure(c, c->der, (size_t)g.der_words * 4 * batch)) != MDX_OK) return rc;
     if ((rc = ensure(c, c->fits, sizeof(PairFit) * (size_t)batch)) != MDX_OK) return rc;
     return MDX_OK;
+}
+
+// Page-locked blocks handed out by mdx_host_alloc: [base, base + bytes).  The trajectory entry
+// writes its outputs straight into them only when a whole output range lies inside one block.
+static std::mutex g_host_mu;
+static std::map<uintptr_t, size_t> g_host_blocks;
+static bool host_block_holds(const void* p, size_t bytes)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    auto it = g_host_blocks.upper_bound(a);
+    if (it == g_host_blocks.begin()) return false;
+    --it;
+    return a >= it->first && bytes <= it->second && a - it->first <= it->second - bytes;
 }
 
 // Residue classes of the grid at each level (see mdx_lk.hip), the class-grouped point order and
@@ -557,10 +573,11 @@ static int lk_err_result(mdx_ctx* c)
     c->lk_fallback[2] += redone;
     HIP_OR_RETURN(c, hipMemsetAsync(c->errw.p, 0, 12, c->stream));
     HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
-    // a give-up is always followed by its level's recompute (launch_lk_v2): one without it would be
-    // a scheduling bug, and its outputs could be wrong
-    if (groups > 0 && redone == 0)
-        return set_err(c, MDX_EHIP, "LK dataflow: %d wait(s) gave up but no level was recomputed", groups);
+    // a give-up (a group wait or a gate) is always followed by its level's recompute (launch_lk_v2):
+    // one without it would be a scheduling bug, and its outputs could be wrong
+    if (groups + gates > 0 && redone == 0)
+        return set_err(c, MDX_EHIP, "LK dataflow: %d wait(s) and %d gate(s) gave up but no level was recomputed",
+                       groups, gates);
     return MDX_OK;
 }
 
@@ -729,6 +746,10 @@ static int run_lk(mdx_ctx* c, const Geometry& g, LkArgs& a, int batch, int w, in
         for (int q = 0; q < 2; q++)
             HIP_OR_RETURN(c, hipMemsetAsync(c->Abuf.as<uint8_t>() + abytes + q * per + qbytes + dbytes + cbytes, 0,
                                             pbytes, c->stream));
+        // the coarsest level may run on the second iteration stream (MDX_LK_XCALL, parity 1), which
+        // does not follow c->stream: finish the zeroing before any launch reads the flags (this runs
+        // only when the flag regions move, i.e. on a reallocation or a layout change)
+        HIP_OR_RETURN(c, hipStreamSynchronize(c->stream));
         c->pflag_mem = c->Abuf.p;
         c->pflag_at = pf_at;
         c->pflag_bytes = pbytes;
@@ -1096,15 +1117,20 @@ static int trajectory_passes(mdx_ctx* c, const Geometry& g, int nimg, int w, int
         t.start_pts = tstart;
         // the caller's outputs in mapped page-locked memory (mdx_host_alloc): the launch writes them
         if (npts > 0 && traj && traj_len && start_pts && vectors) {
-            auto mapped = [](void* p) -> void* {
+            // only whole ranges inside one mdx_host_alloc block qualify (a partly pinned or short
+            // buffer takes the copy path, which reports its errors); pageable memory is never queried
+            const size_t pn = (size_t)npts, nn = (size_t)nimg;
+            auto mapped = [&](void* p, size_t bytes) -> void* {
+                if (!host_block_holds(p, bytes)) return nullptr;
                 hipPointerAttribute_t at{};
                 if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-                    (void)hipGetLastError();   // pageable memory: not an error here
+                    (void)hipGetLastError();
                     return nullptr;
                 }
                 return at.type == hipMemoryTypeHost ? at.devicePointer : nullptr;
             };
-            void* m[4] = {mapped(traj), mapped(traj_len), mapped(start_pts), mapped(vectors)};
+            void* m[4] = {mapped(traj, pn * nn * 8), mapped(traj_len, pn * 4), mapped(start_pts, pn * 8),
+                          mapped(vectors, pn * 32)};
             if (m[0] && m[1] && m[2] && m[3]) {
                 t.htraj = static_cast<float*>(m[0]);
                 t.htlen = static_cast<int*>(m[1]);
@@ -1544,12 +1570,18 @@ extern "C" void* mdx_host_alloc(size_t bytes)
 {
     void* p = nullptr;
     if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    g_host_blocks[reinterpret_cast<uintptr_t>(p)] = bytes ? bytes : 1;
     return p;
 }
 
 extern "C" int mdx_host_free(void* p)
 {
     if (!p) return MDX_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        g_host_blocks.erase(reinterpret_cast<uintptr_t>(p));
+    }
     return hipHostFree(p) == hipSuccess ? MDX_OK : MDX_EHIP;
 }
 
