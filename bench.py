@@ -532,7 +532,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="1080p", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="pairs per step per GPU (default 32 @1080p)")
-    ap.add_argument("--unique", type=int, default=4, help="distinct synthetic pairs per rank")
+    ap.add_argument("--unique", type=int, default=32,
+                    help="distinct synthetic pairs per rank (default 32: every slot of the 1080p batch its own "
+                         "content, BASELINE.md §2)")
     ap.add_argument("--roofline-config", default="4k", choices=sorted(CONFIGS))
     ap.add_argument("--roofline-batch", type=int, default=32)
     ap.add_argument("--no-roofline", action="store_true")

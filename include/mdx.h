@@ -24,7 +24,13 @@
 extern "C" {
 #endif
 
-#define MDX_ABI_VERSION 3    /* 2: mdx_params.call_pipelining, mdx_input_ready; 3: mdx_lk_fallbacks */
+#define MDX_ABI_VERSION 4    /* 2: mdx_params.call_pipelining, mdx_input_ready.
+                                3: mdx_lk_fallbacks; mdx_params grew ransac_iters, ransac_thresh and
+                                   ransac_seed (16 more bytes: a caller built against ABI 2 passes a
+                                   shorter struct); mdx_sync / mdx_device_sync return MDX_OK after an
+                                   LK hand-off that gave up and was recomputed (ABI 2: MDX_EHIP).
+                                4: mdx_abi_version and mdx_params_size: check both at start-up --
+                                   a mismatch means the header and the library differ. */
 
 /* Return codes */
 #define MDX_OK           0
@@ -67,7 +73,7 @@ typedef struct {
     int    thresh;           /* threshold(comp, comp, 190, 255, BINARY) (:127) */
     int    pixel_step;       /* ROS param pixel_step (node.cpp:29; 10 in bag.launch:27) */
     double min_vector_size;  /* ROS param min_vector_size, default 1.0 (node.cpp:44) */
-    int    fit_mode;         /* MDX_FIT_FIRST4 (default) or MDX_FIT_EXTERNAL */
+    int    fit_mode;         /* MDX_FIT_FIRST4 (default), MDX_FIT_EXTERNAL or MDX_FIT_RANSAC */
     int    subspace_precision; /* mdx_fit_subspace arithmetic: MDX_SUBSPACE_F64 (default) or _F32 */
     int    call_pipelining;  /* 0 (default) or 1: consecutive device-entry calls overlap (below) */
     int    ransac_iters;     /* MDX_FIT_RANSAC hypotheses, 1..1024 (default 128) */
@@ -91,6 +97,12 @@ typedef struct mdx_ctx mdx_ctx;
 
 /* Fill params with the reference's constants. */
 void mdx_default_params(mdx_params* p);
+
+/* The ABI version and sizeof(mdx_params) the library was built with.  A caller compares them with
+ * MDX_ABI_VERSION and its own sizeof(mdx_params) before the first mdx_create: the struct is passed
+ * by pointer, so a library newer than the caller's header would read past a shorter struct. */
+int mdx_abi_version(void);
+size_t mdx_params_size(void);
 
 /* Number of grid points for a frame: ceil(w/ps) * ceil(h/ps) (:56-64, x-major order:
  * point k = ix*ny + iy sits at (ix*ps, iy*ps)). */

@@ -38,8 +38,9 @@ EXPORTED = [
     "mdx_srand", "mdx_rand", "mdx_fit_subspace", "mdx_device_pci", "mdx_build_info",
     "mdx_ring_push", "mdx_ring_trajectory", "mdx_ring_reset", "mdx_input_ready",
     "mdx_host_alloc", "mdx_host_free", "mdx_probe_stream3_dev", "mdx_lk_fallbacks",
-    "mdx_debug_div32", "mdx_trajectory_layout",
+    "mdx_debug_div32", "mdx_trajectory_layout", "mdx_abi_version", "mdx_params_size",
 ]
+ABI_VERSION = 4   # include/mdx.h MDX_ABI_VERSION
 
 # csrc/Makefile STAMPED: the files whose bytes the library's provenance stamp hashes, in order
 STAMPED = ["Makefile", "mdx_internal.h", "mdx_api.cpp", "mdx_kernels.hip", "mdx_lk.hip", "mdx_warp.hip",
@@ -111,6 +112,13 @@ def lib() -> C.CDLL:
                        "(hipcc --offload-arch=gfx950); there is no CPU fallback")
     L = C.CDLL(LIB_PATH)
     vp, u8p, f32p, f64p, i32p = C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p
+    L.mdx_abi_version.argtypes = []
+    L.mdx_abi_version.restype = C.c_int
+    L.mdx_params_size.argtypes = []
+    L.mdx_params_size.restype = C.c_size_t
+    if L.mdx_abi_version() != ABI_VERSION or L.mdx_params_size() != C.sizeof(MdxParams):
+        raise MdxError(f"{LIB_PATH}: ABI {L.mdx_abi_version()} / mdx_params {L.mdx_params_size()} B, this binding "
+                       f"expects ABI {ABI_VERSION} / {C.sizeof(MdxParams)} B (rebuild the library)")
     L.mdx_default_params.argtypes = [C.POINTER(MdxParams)]
     L.mdx_default_params.restype = None
     L.mdx_grid_count.argtypes = [C.c_int, C.c_int, C.c_int]

@@ -51,6 +51,17 @@ def test_exports_are_plain_c(mdx):
         assert f in syms, f
 
 
+def test_abi_version_and_params_size(mdx):
+    """mdx_abi_version / mdx_params_size (ABI 4) equal the header's MDX_ABI_VERSION and the
+    binding's mdx_params layout; the binding refuses a library that disagrees."""
+    hdr = open(os.path.join(ROOT, "include", "mdx.h")).read()
+    ver = int(re.search(r"#define MDX_ABI_VERSION (\d+)", hdr).group(1))
+    from motion_detection_amd import _lib
+    L = _lib.lib()
+    assert L.mdx_abi_version() == ver == _lib.ABI_VERSION
+    assert L.mdx_params_size() == C.sizeof(_lib.MdxParams) == 80
+
+
 def test_default_params_are_reference_constants(mdx):
     from motion_detection_amd import _lib
     p = _lib.MdxParams()
