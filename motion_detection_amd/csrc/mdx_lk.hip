@@ -793,9 +793,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
     __shared__ __attribute__((aligned(16))) uint32_t dJ0[256];      // [quad][16]
     __shared__ __attribute__((aligned(16))) uint32_t dJ1[256];
     __shared__ __attribute__((aligned(16))) uint32_t dJ2[NB > 2 ? 256 : 4];
-#if MDX_LK_PROBE_LDS
-    __shared__ __attribute__((aligned(16))) uint32_t dPr[256];
-#endif
 
     const int lane = threadIdx.x, k = lane & 3, slot = lane / LPS, sl = lane % LPS;
     const unsigned long long smask = ((1ull << LPS) - 1) << (slot * LPS);
@@ -1046,11 +1043,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)(U + 256 * c), 16, (int)uoff[c], 0, 0, 0);
                 uoff[c] += rowb;
             }
-#if MDX_LK_PROBE_LDS
-            // measurement probe: one more 1-KiB piece per row (the next plane row's bytes) into a
-            // scratch image nothing reads
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)dPr, 16, (int)(uoff[0] + rowb), 0, 0, 0);
-#endif
         };
         auto dma_j = [&](auto bc) {
             // the quad's taps span 44 bytes: lanes 0-2 carry them, lane 3 stays idle
@@ -1121,24 +1113,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
             __builtin_amdgcn_sched_barrier(0);
             fetch();
 #endif
-#if MDX_LK_PROBE_LDS
-            // measurement probe (not a product path): one more b32 LDS read per element
-            uint32_t pr[10];
-#pragma unroll
-            for (int gi = 0; gi < 10; gi++) pr[gi] = ((__attribute__((address_space(3))) volatile const uint32_t*)lE)[8 * gi + 1];
-#endif
 #pragma unroll
             for (int gi = 0; gi < 10; gi++) {
                 const v2u dc = dcs[gi];
-#if MDX_LK_PROBE_CVT
-                {   // measurement probe (not a product path): two more SDWA converts per element
-                    float d0, d1;
-                    asm volatile("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0"
-                                 : "=v"(d0) : "v"(dc.x));
-                    asm volatile("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1"
-                                 : "=v"(d1) : "v"(dc.x));
-                }
-#endif
                 lo[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
                 // (J*32 - I*32) exactly as the reference's CV_DESCALE(...) - I
                 const int cb = FD ? (int)ccs[gi] : (int)dc.y;
@@ -1148,10 +1125,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                 const f2 f = FD ? __builtin_bit_cast(f2, dc) : f2{(float)(int16_t)dc.x, (float)((int)dc.x >> 16)};
                 acc = acc + f * fd;
             }
-#if MDX_LK_PROBE_LDS
-            asm volatile("" ::"v"(pr[0]), "v"(pr[1]), "v"(pr[2]), "v"(pr[3]), "v"(pr[4]), "v"(pr[5]), "v"(pr[6]),
-                         "v"(pr[7]), "v"(pr[8]), "v"(pr[9]));
-#endif
             asm volatile("" : "+v"(acc));
         };
         if constexpr (NB == 2) {
@@ -1425,6 +1398,10 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         // the even levels' stream (the first level's) and the odd levels'; parity 1 swaps them so
         // that this call's first level does not queue behind the previous call's fit / warp on s
         const bool swap = flow && parity && b.carry;
+#if MDX_LK_NOCARRY
+        // levels in sequence on one stream: the carried points go through next_pts (no per-level arrays)
+        if (!flow) b.carry = nullptr;
+#endif
         hipStream_t s0 = swap ? s2 : s, s1 = swap ? s : s2;
         if (flow) {
             if (hipError_t e = hipMemsetAsync(done, 0, sizeof(int) * ((long long)kMaxLevels * nb + kLkFlagInts) * kCtrPad, s0))
