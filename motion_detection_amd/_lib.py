@@ -112,13 +112,17 @@ def lib() -> C.CDLL:
                        "(hipcc --offload-arch=gfx950); there is no CPU fallback")
     L = C.CDLL(LIB_PATH)
     vp, u8p, f32p, f64p, i32p = C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p
-    L.mdx_abi_version.argtypes = []
-    L.mdx_abi_version.restype = C.c_int
-    L.mdx_params_size.argtypes = []
-    L.mdx_params_size.restype = C.c_size_t
-    if L.mdx_abi_version() != ABI_VERSION or L.mdx_params_size() != C.sizeof(MdxParams):
-        raise MdxError(f"{LIB_PATH}: ABI {L.mdx_abi_version()} / mdx_params {L.mdx_params_size()} B, this binding "
-                       f"expects ABI {ABI_VERSION} / {C.sizeof(MdxParams)} B (rebuild the library)")
+    if hasattr(L, "mdx_abi_version"):
+        L.mdx_abi_version.argtypes = []
+        L.mdx_abi_version.restype = C.c_int
+        L.mdx_params_size.argtypes = []
+        L.mdx_params_size.restype = C.c_size_t
+        if L.mdx_abi_version() != ABI_VERSION or L.mdx_params_size() != C.sizeof(MdxParams):
+            raise MdxError(f"{LIB_PATH}: ABI {L.mdx_abi_version()} / mdx_params {L.mdx_params_size()} B, this binding "
+                           f"expects ABI {ABI_VERSION} / {C.sizeof(MdxParams)} B (rebuild the library)")
+    elif not os.environ.get("MDX_LIB_PATH"):
+        # only developer A/B builds of older revisions (MDX_LIB_PATH) may predate ABI 4
+        raise MdxError(f"{LIB_PATH} predates ABI 4 (no mdx_abi_version): rebuild the library")
     L.mdx_default_params.argtypes = [C.POINTER(MdxParams)]
     L.mdx_default_params.restype = None
     L.mdx_grid_count.argtypes = [C.c_int, C.c_int, C.c_int]

@@ -87,7 +87,6 @@ struct mdx_ctx {
     int traj_ppw = 4;                        // trajectory LK points per wave (MDX_TRAJ_PPW: 1, 2 or 4)
     int lk_impl = 2;                         // 1 = single-kernel LK (k_lk), 2 = class planes
     int lk_g = 0;                            // LK group size: 0 = per level, 4 or 8 (MDX_LK_G)
-    int lk_fd = 0;                           // float derivative class planes (MDX_LK_FD, ClassPlan::fd)
     int lk_sub = 0;                          // > 0: LK sub-batch cap (MDX_LK_SUB, tests)
     bool lk_arows = true;                    // A sums per row strip where the plan allows (MDX_LK_AROWS=0: per group)
     int lk_astrip = 0;                       // grid rows per A-sum strip (MDX_LK_ASTRIP; 0: kAStripRows)
@@ -371,8 +370,7 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
         for (int l = 0; l < g.nlev; l++) {
             ClassLevel& C = P.lv[l];
             C.UH = g.lv[l].h + 79;
-            // float planes stage unions from a multiple of 4 columns: up to 3 more columns
-            C.PW = (g.lv[l].w + kPad + std::max(C.UW + (c->lk_fd ? 4 : 0), 64) + 3) & ~3;
+            C.PW = (g.lv[l].w + kPad + std::max(C.UW, 64) + 3) & ~3;
             // plane rows the band's windows read: first rows v0 = clamp(ipy + 40, 0, UH - 40) of
             // its first and last grid rows (ipy is monotone in gy), 40 rows each
             const float scale = (float)(1. / (1 << l));
@@ -382,14 +380,13 @@ static int ensure_class_plan(mdx_ctx* c, const Geometry& g, int w, int h, int ps
             };
             C.vlo = v0_of(gy0);
             C.vhi = v0_of(gy1 - 1) + kWin;
-            C.class_bytes = (long long)C.UH * C.PW * (c->lk_fd ? 12 : 8);
+            C.class_bytes = (long long)C.UH * C.PW * 8;
             C.off = off;
             off += (long long)C.nrx * C.nry * C.class_bytes;
         }
         // the kernels address a pair's slab with 32-bit buffer offsets
         if (off > 0x7fff0000LL) usable = false;
         P.nch = usable ? 1 : 0;
-        P.fd = c->lk_fd;
         P.bytes_per_pair = (off + 255) / 256 * 256;
         tab.insert(tab.end(), ord.begin(), ord.end());
         if ((rc = ensure(c, c->ctab, tab.size() * sizeof(int16_t))) != MDX_OK) return rc;
@@ -435,7 +432,6 @@ extern "C" mdx_ctx* mdx_create(int device, int max_w, int max_h, int max_batch, 
     c->max_batch = max_batch;
     if (const char* e = std::getenv("MDX_LK_IMPL")) c->lk_impl = std::atoi(e) == 1 ? 1 : 2;
     if (const char* e = std::getenv("MDX_LK_G")) c->lk_g = std::atoi(e);
-    if (const char* e = std::getenv("MDX_LK_FD")) c->lk_fd = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_LK_SUB")) c->lk_sub = std::atoi(e);
     if (const char* e = std::getenv("MDX_LK_AROWS")) c->lk_arows = std::atoi(e) != 0;
     if (const char* e = std::getenv("MDX_LK_ASTRIP")) c->lk_astrip = std::max(0, std::min(std::atoi(e), 64));

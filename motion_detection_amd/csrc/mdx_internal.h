@@ -81,9 +81,6 @@ struct ClassPlan {
     ClassLevel lv[kMaxLevels];
     long long bytes_per_pair;
     int nch;                 // 0: some group's union is wider than 512 columns (single-kernel LK)
-    int fd;                  // 1: float derivative planes (MDX_LK_FD): each plane row is PW float
-                             // pairs (Ix, Iy) then PW int32 C values (12 B per column, unions start
-                             // at multiples of 4 columns); 0: 8-B (D, C) pairs
 };
 
 struct LkClassArgs {

@@ -200,32 +200,11 @@ __device__ __forceinline__ void cls_store(uint4* o, const uint32_t (&dv)[4], con
     __builtin_nontemporal_store(__builtin_bit_cast(v4nt, b), reinterpret_cast<v4nt*>(o) + 1);
 }
 
-// Float derivative planes (ClassPlan::fd, MDX_LK_FD): the same elements with Ix, Iy stored as float
-// (exact: |Ix|, |Iy| <= 4080), so the iterations multiply them without two word-to-float converts
-// per element.  A plane row is PW float pairs (Ix, Iy), then PW int32 C values; row v of a class
-// starts at class base + 12 * PW * v.  Thread j's 4 columns: two 16-B stores of pairs, one of C.
-__device__ __forceinline__ void cls_store_fd(uint8_t* cbase, int v, int PW, int j, const uint32_t (&dv)[4],
-                                             const int (&cv)[4])
-{
-    typedef float v4fnt __attribute__((ext_vector_type(4)));
-    typedef int v4int __attribute__((ext_vector_type(4)));
-    uint8_t* row = cbase + (long long)v * PW * 12;
-    auto fx = [&](int q) { return (float)(int16_t)dv[q]; };
-    auto fy = [&](int q) { return (float)((int)dv[q] >> 16); };
-    const v4fnt a = {fx(0), fy(0), fx(1), fy(1)}, b = {fx(2), fy(2), fx(3), fy(3)};
-    v4fnt* d = reinterpret_cast<v4fnt*>(row) + 2 * j;
-    __builtin_nontemporal_store(a, d);
-    __builtin_nontemporal_store(b, d + 1);
-    const v4int c = {cv[0], cv[1], cv[2], cv[3]};
-    __builtin_nontemporal_store(c, reinterpret_cast<v4int*>(row + 8LL * PW) + j);
-}
-
 // ------------------------------------------------------------------ class planes
 // grid: x -> 4 consecutive plane columns u per thread, y -> plane row v, z -> pair * nclass +
 // class.  Element (u, v) is the window value at level core position (x, y) = (u - 40, v - 40)
 // for the class's bilinear weights: (I*32, Ix, Iy) exactly as LKTrackerInvoker extracts them
 // (CV_DESCALE by W_BITS1-5 = 9 and W_BITS1 = 14).  Outside the level's padded extent: 0.
-template <bool FD>
 __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ pyr1, const uint32_t* __restrict__ der,
                                                   uint8_t* __restrict__ cls_out, LkClassArgs a)
 {
@@ -281,13 +260,9 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
 #pragma unroll
         for (int q = 0; q < 4; q++) cv[q] = 256;
     }
-    if constexpr (FD) {
-        cls_store_fd(base, v, C.PW, j, dv, cv);
-    } else {
-        // (D, C) pairs, row-major: one 8-B element per plane column
-        uint4* o = reinterpret_cast<uint4*>(base) + ((long long)v * C.PW + 4 * j) / 2;
-        cls_store(o, dv, cv);
-    }
+    // (D, C) pairs, row-major: one 8-B element per plane column
+    uint4* o = reinterpret_cast<uint4*>(base) + ((long long)v * C.PW + 4 * j) / 2;
+    cls_store(o, dv, cv);
 }
 
 // Levels with at most 4 residue classes (the finest ones, whose Scharr planes are the largest):
@@ -299,7 +274,6 @@ __global__ __launch_bounds__(256) void k_lk_class(const uint8_t* __restrict__ py
 // k_scharr launch (its plane writes and their reads) is skipped.
 __device__ __forceinline__ int u8_at(const uint32_t (&w)[3], int b) { return (int)((w[b >> 2] >> (8 * (b & 3))) & 255u); }
 
-template <bool FD>
 __global__ __launch_bounds__(256) void k_lk_class_fused(const uint8_t* __restrict__ pyr1, uint8_t* __restrict__ cls_out,
                                                         LkClassArgs a)
 {
@@ -371,12 +345,8 @@ __global__ __launch_bounds__(256) void k_lk_class_fused(const uint8_t* __restric
             });
         }
         uint8_t* base = cls_out + (long long)pair * a.plan.bytes_per_pair + C.off + (long long)cls * C.class_bytes;
-        if constexpr (FD) {
-            cls_store_fd(base, v, C.PW, j, dv, cv);
-        } else {
-            uint4* o = reinterpret_cast<uint4*>(base) + ((long long)v * C.PW + 4 * j) / 2;
-            cls_store(o, dv, cv);
-        }
+        uint4* o = reinterpret_cast<uint4*>(base) + ((long long)v * C.PW + 4 * j) / 2;
+        cls_store(o, dv, cv);
     }
 }
 
@@ -398,18 +368,13 @@ __global__ __launch_bounds__(256) void k_lk_class_fused(const uint8_t* __restric
 // UW is the exact-fit union width (even: a 16-B load carries two pairs); the last load of a
 // slot's row and the last LDS-DMA piece of the wave's row are partial (lane-masked), so no byte
 // beyond the union is moved.
-template <int G, int UW, bool FD = false>
+template <int G, int UW>
 struct LkShape {
     static constexpr int LPS = 4 * G;                         // lanes per slot
     static constexpr int S = 64 / LPS;                        // slots per wave
-    // image columns per slot: float planes start unions at multiples of 4 columns (16-B aligned C
-    // segments), so they stage up to 3 more columns
-    static constexpr int UWI = FD ? UW + 4 : UW;
-    static constexpr int EB = FD ? 12 : 8;                    // image bytes per column (iterations)
-    static constexpr int BYTES = S * UWI * EB;                // the wave's union row image
+    static constexpr int NP = (UW + 2 * LPS - 1) / (2 * LPS); // A pass: 16-B (2-pair) loads per lane and row
+    static constexpr int BYTES = S * UW * 8;                  // the wave's union row image
     static constexpr int ND = (BYTES + 1023) / 1024;          // iterations: LDS-DMA pieces per row
-    static constexpr int ABYTES = S * UWI * 8;                // A sums: (D, C) pairs, or the float D segment alone
-    static constexpr int NDA = (ABYTES + 1023) / 1024;
     static_assert(UW % 2 == 0 && UW >= kWin, "union width");
 };
 
@@ -420,12 +385,10 @@ struct GroupGeom {
     int off;          // the point's first column inside the union
     int v0;           // first window row in the class plane
     uint32_t ubase;   // byte offset in the pair's class slab of the union's first pair, plane row 0
-                      // (float planes: of the union's first (Ix, Iy) pair)
-    uint32_t cbase;   // float planes: byte offset of the union's first C value, plane row 0
 };
 
 // geometry of group g (-1 = none) for lane sl of its slot
-template <int G, int UW, bool FD = false>
+template <int G, int UW>
 __device__ __forceinline__ GroupGeom group_geom(const LkArgs& a, const ClassLevel& C, int level, int g, int sl)
 {
     GroupGeom r;
@@ -449,27 +412,21 @@ __device__ __forceinline__ GroupGeom group_geom(const LkArgs& a, const ClassLeve
     const int m = (1 << level) - 1;
     const int cx = class_of(a.cmap, level, 0, (gx0 * a.pixel_step) & m);
     const int cy = class_of(a.cmap, level, 1, (r.gy * a.pixel_step) & m);
-    int ub = min(max(ipx0 + kPad, 0), C.PW - UW);                  // union start column
+    const int ub = min(max(ipx0 + kPad, 0), C.PW - UW);            // union start column
     r.off = min(max(r.ipx + kPad - ub, 0), UW - kWin);
-    if (FD) {   // the image starts at the multiple of 4 below (16-B aligned C segment)
-        r.off += ub & 3;
-        ub &= ~3;
-    }
     r.v0 = min(max(r.ipy + kPad, 0), C.UH - kWin);
-    const uint32_t cls0 = (uint32_t)(C.off + (long long)(cy * C.nrx + cx) * C.class_bytes);
-    r.ubase = cls0 + 8u * (uint32_t)ub;
-    r.cbase = cls0 + 8u * (uint32_t)C.PW + 4u * (uint32_t)ub;
+    r.ubase = (uint32_t)(C.off + (long long)(cy * C.nrx + cx) * C.class_bytes) + 8u * (uint32_t)ub;
     return r;
 }
 
 // ---- A pass.  grid: x -> wave (S static groups), y -> pair (XCD-remapped as one range).  Each
 // lane loads 2 (D, C) pairs per 16-B load and stages the two D words; the chain reads are D only.
-template <int G, int UW, bool FD>
+template <int G, int UW>
 __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict__ cls, float4* __restrict__ Ab,
                                              int* __restrict__ qctr, int level, int ngroups)
 {
-    using Sh = LkShape<G, UW, FD>;
-    constexpr int LPS = Sh::LPS, S = Sh::S, ND = Sh::NDA, UWI = Sh::UWI;
+    using Sh = LkShape<G, UW>;
+    constexpr int LPS = Sh::LPS, S = Sh::S, ND = Sh::ND;
     constexpr int NB = 3;                                          // row images: NB - 1 rows in flight ahead
     constexpr float FLT_SCALE = 1.f / (1 << 20);
     // [slot][UW][D, C]: the wave's union row images, filled by LDS-DMA like k_lk_iter's; one
@@ -487,20 +444,20 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
     const ClassLevel& C = a.plan.lv[level];
     const Level L = a.g.lv[level];
     const int g = w * S + slot;
-    const GroupGeom q = group_geom<G, UW, FD>(a, C, level, g < ngroups ? g : -1, sl);
+    const GroupGeom q = group_geom<G, UW>(a, C, level, g < ngroups ? g : -1, sl);
     bool ok = q.valid && !(q.ipx < -kWin || q.ipx >= L.w || q.ipy < -kWin || q.ipy >= L.h);
 
     const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cls + (long long)pair * a.plan.bytes_per_pair, a.plan.bytes_per_pair);
-    const uint32_t rowb = (uint32_t)C.PW * (FD ? 12 : 8);
+    const uint32_t rowb = (uint32_t)C.PW * 8;
     // lane L of piece c fills image bytes 1024c + 16L: slot sp's union bytes wb (past the image:
-    // an out-of-range offset, zeros).  Float planes: the (Ix, Iy) segment alone (C is not summed here)
+    // an out-of-range offset, zeros)
     uint32_t uoff[ND];
     {
         const uint32_t mine = q.ubase + (uint32_t)q.v0 * rowb;
 #pragma unroll
         for (int c = 0; c < ND; c++) {
             const int P = 1024 * c + 16 * lane;
-            const int sp = P / (8 * UWI), wb = P % (8 * UWI);
+            const int sp = P / (8 * UW), wb = P % (8 * UW);
             const uint32_t src = (uint32_t)__shfl((int)mine, (sp < S ? sp : 0) * LPS) + (uint32_t)wb;
             uoff[c] = sp < S ? src : 0x80000000u;
         }
@@ -519,7 +476,7 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
             uoff[c] += rowb;
         }
     };
-    const int el = 2 * (slot * UWI + q.off + k);
+    const int el = 2 * (slot * UW + q.off + k);
 
     // lane k owns SSE lane k (columns 4g+k), rows in order; ((P0+P1)+P2)+P3 across the quad
     f2 sd = {0.f, 0.f};
@@ -536,19 +493,13 @@ __global__ __launch_bounds__(64) void k_lk_A(LkArgs a, const uint8_t* __restrict
         if constexpr (y + PF < kWin) dma(std::integral_constant<int, (y + PF) % NB>{});
         __builtin_amdgcn_sched_barrier(0);
         lds_u2v* lE = (lds_u2v*)(ibuf(std::integral_constant<int, y % NB>{}) + el);
-        f2 fs[10];
+        uint32_t dw[10];
 #pragma unroll
-        for (int gi = 0; gi < 10; gi++) {   // the D word (float planes: the (Ix, Iy) pair) of column q.off + k + 4 gi
-            if constexpr (FD) {
-                fs[gi] = __builtin_bit_cast(f2, lE[4 * gi]);
-            } else {
-                const uint32_t d = lE[4 * gi].x;
-                fs[gi] = f2{(float)(int16_t)d, (float)((int)d >> 16)};
-            }
-        }
+        for (int gi = 0; gi < 10; gi++) dw[gi] = lE[4 * gi].x;      // the D word of pair q.off + k + 4 gi
 #pragma unroll
         for (int gi = 0; gi < 10; gi++) {
-            const f2 f = fs[gi];
+            const uint32_t d = dw[gi];
+            const f2 f = {(float)(int16_t)d, (float)((int)d >> 16)};
             // the reference rounds each product to float, then adds (_mm_mul_ps, _mm_add_ps).
             // |Ix|, |Iy| <= 4080 (Scharr of u8, interpolated), so every product is below 2^24 and
             // exact in float: one fused multiply-add rounds exactly like the two operations
@@ -599,12 +550,12 @@ __device__ __forceinline__ float4 lk_A_result(f2 sd, float s12, bool ok, float m
 // its first row to its 40th, then is finished like k_lk_A's.  Each window's chains see exactly
 // k_lk_A's operands in k_lk_A's order, so the sums are the same bits.
 // grid: x -> (strip, column-group wave), y -> pair (XCD-remapped as one range)
-template <int G, int UW, int NW, bool FD>
+template <int G, int UW, int NW>
 __global__ __launch_bounds__(64) void k_lk_A_rows(LkArgs a, const uint8_t* __restrict__ cls, float4* __restrict__ Ab,
                                                   int* __restrict__ qctr, int level, int ncg)
 {
-    using Sh = LkShape<G, UW, FD>;
-    constexpr int LPS = Sh::LPS, S = Sh::S, ND = Sh::NDA, UWI = Sh::UWI;
+    using Sh = LkShape<G, UW>;
+    constexpr int LPS = Sh::LPS, S = Sh::S, ND = Sh::ND;
     __shared__ __attribute__((aligned(16))) uint32_t img0[ND * 256];
     __shared__ __attribute__((aligned(16))) uint32_t img1[ND * 256];
     __shared__ __attribute__((aligned(16))) uint32_t img2[ND * 256];
@@ -634,26 +585,22 @@ __global__ __launch_bounds__(64) void k_lk_A_rows(LkArgs a, const uint8_t* __res
     const int ipx0 = (int)floorf((float)((gx0 >= 0 ? gx0 : 0) * a.pixel_step) * scale - 19.5f);
     const int cx = class_of(a.cmap, level, 0, ((gx0 >= 0 ? gx0 : 0) * a.pixel_step) & m);
     const int cy = class_of(a.cmap, level, 1, (gy0 * a.pixel_step) & m);
-    int ub = min(max(ipx0 + kPad, 0), C.PW - UW);
-    int off = min(max(ipx + kPad - ub, 0), UW - kWin);
-    if (FD) {   // group_geom's image start
-        off += ub & 3;
-        ub &= ~3;
-    }
+    const int ub = min(max(ipx0 + kPad, 0), C.PW - UW);
+    const int off = min(max(ipx + kPad - ub, 0), UW - kWin);
     const uint32_t ubase = (uint32_t)(C.off + (long long)(cy * C.nrx + cx) * C.class_bytes) + 8u * (uint32_t)ub;
     const int ipy0 = (int)floorf((float)(gy0 * a.pixel_step) * scale - 19.5f);
     const int v00 = min(max(ipy0 + kPad, 0), C.UH - kWin);
     const int R = (nr - 1) * asp + kWin;                           // plane rows of the strip
 
     const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cls + (long long)pair * a.plan.bytes_per_pair, a.plan.bytes_per_pair);
-    const uint32_t rowb = (uint32_t)C.PW * (FD ? 12 : 8);
+    const uint32_t rowb = (uint32_t)C.PW * 8;
     uint32_t uoff[ND];
     {
         const uint32_t mine = ubase + (uint32_t)v00 * rowb;
 #pragma unroll
         for (int c = 0; c < ND; c++) {
             const int P = 1024 * c + 16 * lane;
-            const int sp = P / (8 * UWI), wb = P % (8 * UWI);
+            const int sp = P / (8 * UW), wb = P % (8 * UW);
             const uint32_t src = (uint32_t)__shfl((int)mine, (sp < S ? sp : 0) * LPS) + (uint32_t)wb;
             uoff[c] = sp < S ? src : 0x80000000u;
         }
@@ -672,7 +619,7 @@ __global__ __launch_bounds__(64) void k_lk_A_rows(LkArgs a, const uint8_t* __res
             uoff[c] += rowb;
         }
     };
-    const int el = 2 * (slot * UWI + off + k);
+    const int el = 2 * (slot * UW + off + k);
 
     // window slots: rin[s] = rows the slot's window has summed (-1: idle), jw[s] = its strip row
     f2 sd[NW];
@@ -701,17 +648,12 @@ __global__ __launch_bounds__(64) void k_lk_A_rows(LkArgs a, const uint8_t* __res
         if (t + 2 < R) dma(std::integral_constant<int, (decltype(bc)::value + 2) % 3>{});
         __builtin_amdgcn_sched_barrier(0);
         lds_u2v* lE = (lds_u2v*)(ibuf(bc) + el);
+        uint32_t dw[10];
+#pragma unroll
+        for (int gi = 0; gi < 10; gi++) dw[gi] = lE[4 * gi].x;
         f2 f[10];
-        if constexpr (FD) {
 #pragma unroll
-            for (int gi = 0; gi < 10; gi++) f[gi] = __builtin_bit_cast(f2, lE[4 * gi]);
-        } else {
-            uint32_t dw[10];
-#pragma unroll
-            for (int gi = 0; gi < 10; gi++) dw[gi] = lE[4 * gi].x;
-#pragma unroll
-            for (int gi = 0; gi < 10; gi++) f[gi] = f2{(float)(int16_t)dw[gi], (float)((int)dw[gi] >> 16)};
-        }
+        for (int gi = 0; gi < 10; gi++) f[gi] = f2{(float)(int16_t)dw[gi], (float)((int)dw[gi] >> 16)};
         if (nextj < nr && t == nextj * asp) {   // window nextj starts here (slot nextj % NW is free)
             static_for<0, NW>([&](auto sc) {
                 constexpr int s = decltype(sc)::value;
@@ -769,17 +711,16 @@ __global__ __launch_bounds__(64) void k_lk_A_rows(LkArgs a, const uint8_t* __res
 // A lane then reads its 10 chain pairs with ds_read_b64 (kept apart: a merged ds_read2_b64
 // would halve the LDS rate) and the quad's J dwords with three ds_read_b128.  D and C travel as
 // one pair, so a chain element is one 2-cycle LDS access (it was two read2_b32 halves).
-template <int G, int UW, bool FD>
+template <int G, int UW, bool DF>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWavesPerEU, 8))) void k_lk_iter(
     LkArgs a, const uint8_t* __restrict__ cls, const float4* __restrict__ Ab, int* __restrict__ qctr, int level,
     int ngroups, int batch)
 {
-    using Sh = LkShape<G, UW, FD>;
-    constexpr int LPS = Sh::LPS, S = Sh::S, ND = Sh::ND, UWI = Sh::UWI, EB = Sh::EB;
+    using Sh = LkShape<G, UW>;
+    constexpr int LPS = Sh::LPS, S = Sh::S, ND = Sh::ND;
     constexpr float HALFW = 19.5f;
     constexpr float FLT_SCALE = 1.f / (1 << 20);
-    constexpr int IW = Sh::BYTES / 4;                             // dwords per union row image
-    // [slot][UW][D, C] pairs; float planes: [slot]([UWI][Ix, Iy], [UWI] C)
+    constexpr int UB = S * UW;                                    // (D, C) pairs per union buffer
     // Row buffers: window rows are fetched NB - 1 ahead of the row being summed.  One __shared__
     // array per buffer, so that the compiler sees a row's LDS reads and the DMA into another
     // buffer as disjoint: with one [NB][...] array it put a vmcnt(0) -- a wait for the DMA just
@@ -787,9 +728,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
     constexpr int NB = MDX_LK_NB;
     static_assert(NB == 2 || NB == 3, "row buffers");
     static_assert(kWin == 40, "row schedule (20 row pairs; 6 row sextets + 4)");
-    __shared__ __attribute__((aligned(16))) uint32_t dU0[IW];
-    __shared__ __attribute__((aligned(16))) uint32_t dU1[IW];
-    __shared__ __attribute__((aligned(16))) uint32_t dU2[NB > 2 ? IW : 4];
+    __shared__ __attribute__((aligned(16))) uint32_t dU0[2 * UB];   // [slot][UW][D, C]
+    __shared__ __attribute__((aligned(16))) uint32_t dU1[2 * UB];
+    __shared__ __attribute__((aligned(16))) uint32_t dU2[NB > 2 ? 2 * UB : 4];
     __shared__ __attribute__((aligned(16))) uint32_t dJ0[256];      // [quad][16]
     __shared__ __attribute__((aligned(16))) uint32_t dJ1[256];
     __shared__ __attribute__((aligned(16))) uint32_t dJ2[NB > 2 ? 256 : 4];
@@ -798,36 +739,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
     const unsigned long long smask = ((1ull << LPS) - 1) << (slot * LPS);
     const unsigned long long t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const int xcd = blockIdx.x & 7;
+    // DF = false (levels in sequence, no dataflow, no recompute): the hand-off, give-up and recompute
+    // code below folds away, so the plain kernel carries none of it
+    int* const a_done = DF ? a.done : nullptr;
+    int* const a_lflags = DF ? a.lflags : nullptr;
+    const int a_redo = DF ? a.redo : 0;
+    const int dep_groups = DF ? a.dep_groups : 0;
+    const int dep_points = DF ? a.dep_points : 0;
     const long long T = (long long)batch * ngroups;
     const long long cb = T * xcd / 8, ce = T * (xcd + 1) / 8;     // this XCD's range of the work list
     const int p0 = (int)(cb / ngroups);
     const uint32_t off0 = (uint32_t)(cb - (long long)p0 * ngroups);   // cb's group within pair p0
     const int np = ce > cb ? (int)((ce - 1) / ngroups) - p0 + 1 : 1;
     int* ctr = qctr + (level * 8 + xcd) * kCtrPad;
-    if (a.redo) {
+    if (a_redo) {
         // the level's recompute: only if it gave up, or the coarser level was recomputed (its
         // carried points changed after this level read them); levels then run in sequence
-        int need = __hip_atomic_load(a.lflags + (kLkFlagGiveup + level) * kCtrPad, __ATOMIC_RELAXED,
+        int need = __hip_atomic_load(a_lflags + (kLkFlagGiveup + level) * kCtrPad, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
         if (level < a.maxl)
-            need |= __hip_atomic_load(a.lflags + (kLkFlagRedone + level + 1) * kCtrPad, __ATOMIC_RELAXED,
+            need |= __hip_atomic_load(a_lflags + (kLkFlagRedone + level + 1) * kCtrPad, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);
         if (!need) return;
         if (blockIdx.x == 0 && lane == 0) {
-            __hip_atomic_store(a.lflags + (kLkFlagRedone + level) * kCtrPad, 1, __ATOMIC_RELAXED,
+            __hip_atomic_store(a_lflags + (kLkFlagRedone + level) * kCtrPad, 1, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(a.err + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        ctr = a.lflags + (kLkFlagQueue + level * 8 + xcd) * kCtrPad;
+        ctr = a_lflags + (kLkFlagQueue + level * 8 + xcd) * kCtrPad;
     }
     // this level's give-up flag (dataflow): set by the first wait that gives up or by the gate
-    int* const giveup = a.lflags ? a.lflags + (kLkFlagGiveup + level) * kCtrPad : nullptr;
+    int* const giveup = a_lflags ? a_lflags + (kLkFlagGiveup + level) * kCtrPad : nullptr;
     const ClassLevel& C = a.plan.lv[level];
     const Level L = a.g.lv[level];
     // buffer addressing: descriptors over the range's class slabs and next-frame pyramids (the
     // host keeps them below 2 GB), 32-bit lane offsets
     const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cls + (long long)p0 * a.plan.bytes_per_pair, np * a.plan.bytes_per_pair);
-    const uint32_t rowb = (uint32_t)C.PW * EB;
+    const uint32_t rowb = (uint32_t)C.PW * 8;
     const int pitch = L.pitch;
     const __amdgpu_buffer_rsrc_t jrs = buf_rsrc(a.pyr2 + (long long)p0 * a.g.img_bytes, np * a.g.img_bytes);
     const uint32_t jbase = (uint32_t)(L.img_off + L.core());
@@ -856,25 +804,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                 a.dbg[((long long)pair * a.g.nlev + level) * a.npts + pt] = make_float4(npx, npy, (float)iters, (float)status);
             const float2 v = make_float2(npx, npy);
             float* dst = (a.carry && level > 0) ? a.carry + level * a.carry_lstride : a.next_pts;
-            if (a.done)   // read by the next level's launch while this one runs: write-through (sc1)
+            if (a_done)   // read by the next level's launch while this one runs: write-through (sc1)
                 __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst) + po,
                                    __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else
                 reinterpret_cast<float2*>(dst)[po] = v;
             if (level == 0) a.status[po] = (uint8_t)status;
         }
-        if (a.done && level > 0) {
+        if (a_done && level > 0) {
             // the group's points have their level result: once this wave's stores are done, one
             // lane of the slot counts the group for its pair (MI355X_MICROARCH.md hand-off: sc1
             // stores, vmcnt(0), agent atomic; the reader polls and loads sc1) -- or, per-point
             // dataflow, each point's lane stamps the point with the call's epoch
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (a.dep_points) {
+            if (dep_points) {
                 if (q.valid && k == 0)
                     __hip_atomic_store(a.pflags + level * a.pf_lstride + po, a.epoch, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             } else if (sl == 0) {
-                __hip_atomic_fetch_add(a.done + (level * a.done_stride + pair) * kCtrPad, 1, __ATOMIC_RELAXED,
+                __hip_atomic_fetch_add(a_done + (level * a.done_stride + pair) * kCtrPad, 1, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
         }
@@ -896,9 +844,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                     // position in the XCD's range relative to its first pair: 32-bit division
                     const uint32_t r = off0 + (uint32_t)gi, dp = r / (uint32_t)ngroups;
                     pair = p0 + (int)dp;
-                    q = group_geom<G, UW, FD>(a, C, level, (int)(r - dp * (uint32_t)ngroups), sl);
+                    q = group_geom<G, UW>(a, C, level, (int)(r - dp * (uint32_t)ngroups), sl);
                     q.ubase += (uint32_t)((long long)(pair - p0) * a.plan.bytes_per_pair);
-                    q.cbase += (uint32_t)((long long)(pair - p0) * a.plan.bytes_per_pair);
                     jrel = (uint32_t)((long long)(pair - p0) * a.g.img_bytes);
                     pt = q.gx * a.ny + q.gy;
                     po = (long long)pair * a.npts + pt;
@@ -913,8 +860,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                     } else {
                         float2 p = make_float2(0.f, 0.f);
                         const float* src = a.carry ? a.carry + (level + 1) * a.carry_lstride : a.next_pts;
-                        const bool wait_pt = a.dep_points && level < a.maxl;
-                        if (a.dep_groups || wait_pt) {
+                        const bool wait_pt = dep_points && level < a.maxl;
+                        if (dep_groups || wait_pt) {
                             // dataflow: the coarser level may still run -- wait until every group of
                             // this pair has retired there (per-point dataflow: until this lane's
                             // point has; bounded: the coarser level's waves are resident and drain
@@ -927,8 +874,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                                 // polls back off (1 .. 16 sleeps between loads): thousands of
                                 // waiting waves polling one line would load its L2 channel
                                 const int* d = wait_pt ? a.pflags + (level + 1) * a.pf_lstride + po
-                                                       : a.done + ((level + 1) * a.done_stride + pair) * kCtrPad;
-                                const int target = wait_pt ? a.epoch : a.dep_groups;
+                                                       : a_done + ((level + 1) * a.done_stride + pair) * kCtrPad;
+                                const int target = wait_pt ? a.epoch : dep_groups;
                                 int slept = 0, gap = 1;
                                 bool mine = false;
                                 if (a.spin_max < 0) mine = true;   // fault injection (tests)
@@ -969,7 +916,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                     }
                     act = Dinv > 0.f;   // real point, window inside, eigenvalue / determinant tests passed
                     // an abandoned level retires its groups at once (its recompute redoes them)
-                    if ((a.dep_groups || a.dep_points) && (__ballot(gave_up) & smask)) act = false;
+                    if ((dep_groups || dep_points) && (__ballot(gave_up) & smask)) act = false;
                     status = (level == 0 && q.valid && !act) ? 0 : 1;
                     nx = npx - HALFW;
                     ny = npy - HALFW;
@@ -1009,18 +956,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
         uint32_t uoff[ND];
         {
             const uint32_t mine = q.ubase + (uint32_t)q.v0 * rowb;
-            const uint32_t minec = q.cbase + (uint32_t)q.v0 * rowb;
 #pragma unroll
             for (int c = 0; c < ND; c++) {
                 const int P = 1024 * c + 16 * lane;
-                const int sp = P / (EB * UWI), wb = P % (EB * UWI);
-                if constexpr (FD) {   // the slot's (Ix, Iy) segment, then its C segment
-                    const uint32_t dsrc = (uint32_t)__shfl((int)mine, sp * LPS);
-                    const uint32_t csrc = (uint32_t)__shfl((int)minec, sp * LPS);
-                    uoff[c] = wb < 8 * UWI ? dsrc + (uint32_t)wb : csrc + (uint32_t)(wb - 8 * UWI);
-                } else {
-                    uoff[c] = (uint32_t)__shfl((int)mine, sp * LPS) + (uint32_t)wb;
-                }
+                const int sp = P / (8 * UW), wb = P % (8 * UW);
+                uoff[c] = (uint32_t)__shfl((int)mine, sp * LPS) + (uint32_t)wb;
             }
         }
         auto ubuf = [&](auto bc) -> uint32_t* {
@@ -1049,9 +989,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
             if (k < 3) __builtin_amdgcn_raw_ptr_buffer_load_lds(jrs, (lds_ptr)jbuf(bc), 16, (int)joff, 0, 0, 0);
             joff += (uint32_t)pitch;
         };
-        const int jl = (lane >> 2) * 16;
-        const int el = FD ? slot * 3 * UWI + 2 * (q.off + k) : 2 * (slot * UW + q.off + k);
-        const int elc = slot * 3 * UWI + 2 * UWI + q.off + k;    // float planes: the C value
+        const int jl = (lane >> 2) * 16, el = 2 * (slot * UW + q.off + k);
         auto read_j = [&](auto bc, uint32_t (&rj)[11]) {
             lds_u4v* lJ = (lds_u4v*)(jbuf(bc) + jl);
             const v4u j0 = lJ[0], j1 = lJ[1], j2 = lJ[2];
@@ -1102,13 +1040,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
             v2u dcs[10];
 #pragma unroll
             for (int gi = 0; gi < 10; gi++) dcs[gi] = lE[4 * gi];
-            uint32_t ccs[10];
-            if constexpr (FD) {
-                typedef __attribute__((address_space(3))) volatile const uint32_t lds_u1v;
-                lds_u1v* lC = (lds_u1v*)(ubuf(std::integral_constant<int, R % NB>{}) + elc);
-#pragma unroll
-                for (int gi = 0; gi < 10; gi++) ccs[gi] = lC[4 * gi];
-            }
 #if MDX_LK_RFIRST
             __builtin_amdgcn_sched_barrier(0);
             fetch();
@@ -1118,11 +1049,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
                 const v2u dc = dcs[gi];
                 lo[gi] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(rj[gi + 1], rj[gi], sel));
                 // (J*32 - I*32) exactly as the reference's CV_DESCALE(...) - I
-                const int cb = FD ? (int)ccs[gi] : (int)dc.y;
-                const int jd = __builtin_amdgcn_sdot2(up[gi], W0, __builtin_amdgcn_sdot2(lo[gi], W1, cb, false),
+                const int jd = __builtin_amdgcn_sdot2(up[gi], W0, __builtin_amdgcn_sdot2(lo[gi], W1, (int)dc.y, false),
                                                       false) >> 9;
                 const float fd = (float)jd;
-                const f2 f = FD ? __builtin_bit_cast(f2, dc) : f2{(float)(int16_t)dc.x, (float)((int)dc.x >> 16)};
+                const f2 f = {(float)(int16_t)dc.x, (float)((int)dc.x >> 16)};
                 acc = acc + f * fd;
             }
             asm volatile("" : "+v"(acc));
@@ -1233,18 +1163,18 @@ __global__ __launch_bounds__(64) void k_lk_gate(const int* __restrict__ qctr, lo
 
 // persistent waves for k_lk_iter: what the current device keeps resident at once (cached per
 // device; contexts on several devices may launch from several host threads)
-template <int G, int UW, bool FD>
+template <int G, int UW, bool DF>
 static int lk_iter_resident()
 {
     constexpr int kDevs = 64;
-    static std::atomic<int> cached[kDevs];   // one table per kernel instantiation
+    static std::atomic<int> cached[kDevs];
     int dev = 0;
     (void)hipGetDevice(&dev);
     int v = dev >= 0 && dev < kDevs ? cached[dev].load(std::memory_order_relaxed) : 0;
     if (!v) {
         int ncu = 0, nb = 0;
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lk_iter<G, UW, FD>, 64, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lk_iter<G, UW, DF>, 64, 0);
         v = std::max(1, ncu) * std::max(1, nb);
         if (dev >= 0 && dev < kDevs) cached[dev].store(v, std::memory_order_relaxed);
     }
@@ -1257,16 +1187,16 @@ static int lk_groups(const LkArgs& a, int l)
     return (a.plan.lv[l].nxp / G) * a.nyg;
 }
 
-template <int G, int UW, bool FD>
+template <int G, int UW>
 static void launch_A(hipStream_t s, int batch, const LkArgs& a, const uint8_t* cls, float4* Ab, int* qctr, int l)
 {
     constexpr int S = LkShape<G, UW>::S;
     const int ngroups = lk_groups<G, UW>(a, l);
     const dim3 grid((ngroups + S - 1) / S, batch);
-    hipLaunchKernelGGL((k_lk_A<G, UW, FD>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups);
+    hipLaunchKernelGGL((k_lk_A<G, UW>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups);
 }
 
-template <int G, int UW, bool FD>
+template <int G, int UW>
 static void launch_A_rows(hipStream_t s, int batch, const LkArgs& a, const uint8_t* cls, float4* Ab, int* qctr, int l)
 {
     constexpr int S = LkShape<G, UW>::S;
@@ -1274,12 +1204,12 @@ static void launch_A_rows(hipStream_t s, int batch, const LkArgs& a, const uint8
     const int ncg = C.nxp / G;
     const dim3 grid(((ncg + S - 1) / S) * C.nstrip, batch);
     if (C.asp >= 10)
-        hipLaunchKernelGGL((k_lk_A_rows<G, UW, 4, FD>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ncg);
+        hipLaunchKernelGGL((k_lk_A_rows<G, UW, 4>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ncg);
     else
-        hipLaunchKernelGGL((k_lk_A_rows<G, UW, 8, FD>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ncg);
+        hipLaunchKernelGGL((k_lk_A_rows<G, UW, 8>), grid, dim3(64), 0, s, a, cls, Ab, qctr, l, ncg);
 }
 
-template <int G, int UW, bool FD>
+template <int G, int UW>
 static void launch_iter(hipStream_t s, int batch, const LkArgs& a, const uint8_t* cls, const float4* Ab, int* qctr,
                         int l)
 {
@@ -1290,11 +1220,13 @@ static void launch_iter(hipStream_t s, int batch, const LkArgs& a, const uint8_t
     // (which must be done before that level's launch can start) and for the coarser level's
     // launch that this one may wait on
     const int need = (int)std::min<long long>(((long long)batch * ngroups + S - 1) / S, 1 << 30);
-    int res = lk_iter_resident<G, UW, FD>();
+    const bool df = a.done || a.redo || a.lflags || a.dep_groups || a.dep_points;
+    int res = df ? lk_iter_resident<G, UW, true>() : lk_iter_resident<G, UW, false>();
     if (a.done) res = res * std::min(std::max(a.flow_cap, 10), 100) / 100;   // the context's (MDX_LK_CAP)
     int W = std::max(8, std::min((need + 7) / 8, res / 8) * 8);
     if (a.redo) W = std::max(8, std::min(W, kLkRedoWaves));
-    hipLaunchKernelGGL((k_lk_iter<G, UW, FD>), dim3(W), dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups, batch);
+    if (df) hipLaunchKernelGGL((k_lk_iter<G, UW, true>), dim3(W), dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups, batch);
+    else hipLaunchKernelGGL((k_lk_iter<G, UW, false>), dim3(W), dim3(64), 0, s, a, cls, Ab, qctr, l, ngroups, batch);
 }
 
 hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batch, const LkArgs& a, uint8_t* cls,
@@ -1348,8 +1280,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             if (C.nrx * C.nry <= 4) {
                 // the finest levels: derivatives computed inside the class kernel, no Scharr planes
                 const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.vhi - C.vlo, nb);
-                if (a.plan.fd) hipLaunchKernelGGL(k_lk_class_fused<true>, grid, dim3(64), 0, sa, b.pyr1, bcls, ca);
-                else hipLaunchKernelGGL(k_lk_class_fused<false>, grid, dim3(64), 0, sa, b.pyr1, bcls, ca);
+                hipLaunchKernelGGL(k_lk_class_fused, grid, dim3(64), 0, sa, b.pyr1, bcls, ca);
             } else {
                 const dim3 grid(((a.g.lv[l].w + 2 * kPad) / 4 + 63) / 64, C.vhi - C.vlo, nb * C.nrx * C.nry);
                 // this level's Scharr planes (the caller left them to us): on the aux stream, so
@@ -1357,21 +1288,15 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
                 // (the derivative rows the class planes read: v, v + 1 for plane rows v in [vlo, vhi))
                 if (hipError_t e = launch_scharr(sa, nb, b.pyr1, const_cast<uint32_t*>(b.der), a.g, l, C.vlo, C.vhi + 1))
                     return e;
-                if (a.plan.fd) hipLaunchKernelGGL(k_lk_class<true>, grid, dim3(64), 0, sa, b.pyr1, b.der, bcls, ca);
-                else hipLaunchKernelGGL(k_lk_class<false>, grid, dim3(64), 0, sa, b.pyr1, b.der, bcls, ca);
+                hipLaunchKernelGGL(k_lk_class, grid, dim3(64), 0, sa, b.pyr1, b.der, bcls, ca);
             }
             float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             const int G = C.G, UW = C.UW;
             switch (G * 1000 + UW) {
 #define LK_CASE(g, uw)                                                              \
     case g * 1000 + uw:                                                             \
-        if (a.plan.fd) {                                                            \
-            if (C.asp) launch_A_rows<g, uw, true>(sa, nb, b, bcls, bA, bq, l);     \
-            else launch_A<g, uw, true>(sa, nb, b, bcls, bA, bq, l);                \
-        } else {                                                                    \
-            if (C.asp) launch_A_rows<g, uw, false>(sa, nb, b, bcls, bA, bq, l);    \
-            else launch_A<g, uw, false>(sa, nb, b, bcls, bA, bq, l);               \
-        }                                                                           \
+        if (C.asp) launch_A_rows<g, uw>(sa, nb, b, bcls, bA, bq, l);               \
+        else launch_A<g, uw>(sa, nb, b, bcls, bA, bq, l);                          \
         break;
                 LK_SHAPES
 #undef LK_CASE
@@ -1398,10 +1323,6 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
         // the even levels' stream (the first level's) and the odd levels'; parity 1 swaps them so
         // that this call's first level does not queue behind the previous call's fit / warp on s
         const bool swap = flow && parity && b.carry;
-#if MDX_LK_NOCARRY
-        // levels in sequence on one stream: the carried points go through next_pts (no per-level arrays)
-        if (!flow) b.carry = nullptr;
-#endif
         hipStream_t s0 = swap ? s2 : s, s1 = swap ? s : s2;
         if (flow) {
             if (hipError_t e = hipMemsetAsync(done, 0, sizeof(int) * ((long long)kMaxLevels * nb + kLkFlagInts) * kCtrPad, s0))
@@ -1442,11 +1363,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
             }
             const float4* bA = Ab + ((long long)l * batch + p) * a.npts;
             switch (C.G * 1000 + C.UW) {
-#define LK_CASE(g, uw)                                                                   \
-    case g * 1000 + uw:                                                                  \
-        if (a.plan.fd) launch_iter<g, uw, true>(st, nb, bl, bcls, bA, bq, l);            \
-        else launch_iter<g, uw, false>(st, nb, bl, bcls, bA, bq, l);                     \
-        break;
+#define LK_CASE(g, uw) case g * 1000 + uw: launch_iter<g, uw>(st, nb, bl, bcls, bA, bq, l); break;
                 LK_SHAPES
 #undef LK_CASE
             default: return hipErrorInvalidValue;
@@ -1464,11 +1381,7 @@ hipError_t launch_lk_v2(hipStream_t s, hipStream_t aux, hipEvent_t* ev, int batc
                     br.redo = 1;
                     br.dbg = nullptr;
                     switch (C.G * 1000 + C.UW) {
-#define LK_CASE(g, uw)                                                                   \
-    case g * 1000 + uw:                                                                  \
-        if (a.plan.fd) launch_iter<g, uw, true>(st, nb, br, bcls, bA, bq, l);            \
-        else launch_iter<g, uw, false>(st, nb, br, bcls, bA, bq, l);                     \
-        break;
+#define LK_CASE(g, uw) case g * 1000 + uw: launch_iter<g, uw>(st, nb, br, bcls, bA, bq, l); break;
                         LK_SHAPES
 #undef LK_CASE
                     default: return hipErrorInvalidValue;

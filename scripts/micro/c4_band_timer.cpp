@@ -64,15 +64,17 @@ int main(int argc, char** argv)
                 return false;
         return true;
     };
-    // the records every band's fit sees: this band's own record in all K slots (a real fit)
-    for (auto& x : cs) {
-        if (mdx_band_flow_dev(x.c, x.i1, x.i2, w, hh, w * 3, MDX_FMT_RGB8, y0, y1, x.np, x.st, nullptr, x.cand) < 0)
+    // the records every band's fit sees: all K bands' real records (bench.py's exchange), made once
+    std::vector<unsigned char> recs(96 * K);
+    for (int k = 0; k < K; k++) {
+        const int b0 = (hh * k) / K, b1 = (hh * (k + 1)) / K;
+        if (mdx_band_flow_dev(cs[0].c, cs[0].i1, cs[0].i2, w, hh, w * 3, MDX_FMT_RGB8, b0, b1, cs[0].np, cs[0].st,
+                              nullptr, cs[0].cand) < 0)
             return 4;
-        mdx_device_sync(x.c);
-        unsigned char rec[96];
-        mdx_memcpy_d2h(x.c, rec, x.cand, 96);
-        for (int k = 0; k < K; k++) mdx_memcpy_h2d(x.c, (unsigned char*)x.cands + 96 * k, rec, 96);
+        mdx_device_sync(cs[0].c);
+        mdx_memcpy_d2h(cs[0].c, recs.data() + 96 * k, cs[0].cand, 96);
     }
+    for (auto& x : cs) mdx_memcpy_h2d(x.c, x.cands, recs.data(), recs.size());
     for (int i = 0; i < 3; i++) if (!rep()) { std::fprintf(stderr, "call: %s\n", mdx_last_error(cs[0].c)); return 4; }
     for (auto& x : cs) mdx_device_sync(x.c);
     const auto t0 = std::chrono::steady_clock::now();
