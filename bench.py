@@ -532,6 +532,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="1080p", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="pairs per step per GPU (default 32 @1080p)")
+    ap.add_argument("--cold-idle", type=float, default=1.0,
+                    help="roofline leg: idle seconds before the timed cold burst (reported as roofline.cold_burst)")
     ap.add_argument("--unique", type=int, default=32,
                     help="distinct synthetic pairs per rank (default 32: every slot of the 1080p batch its own "
                          "content, BASELINE.md §2)")
@@ -761,7 +763,19 @@ def main():
         # 180-190 -> 141 us over its first ~120 launches on the same inputs, the copy probe flat at
         # 121 us: profiles/r05_warp_transient.txt), so each leg is timed after roofline_warmup launches
         rwarm = max(2, args.warmup, args.roofline_warmup)
+        cold_ms = None
         if args.roofline_h != "projective":
+            # the cold burst, reported beside the warmed figure: the first --steps launches after
+            # --cold-idle seconds of idle (the warmup's first launches)
+            rctx.device_sync()
+            time.sleep(max(0.0, args.cold_idle))
+            rctx.enable_timing(True)
+            for _ in range(args.steps):
+                rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
+            rctx.device_sync()
+            cs0 = rctx.stage_ms()
+            cold_ms = cs0["warp_diff"] / max(cs0["calls"], 1)
+            rctx.enable_timing(False)
             for _ in range(rwarm):
                 rctx.warp_diff_dev(RB, e1, e2, rw, rh, rw, rw * rh, eH, eM)
             rctx.device_sync()
@@ -821,6 +835,11 @@ def main():
                     workload=f"{rw}x{rh} gray, {RB} pairs per launch, true H (affine), 3 B/px algorithmic",
                     avg_launch_us=round(launch_ms * 1e3, 2) if launch_ms else None,
                     timed_launches=args.steps, warmup_launches=rwarm,
+                    cold_burst=(dict(avg_launch_us=round(cold_ms * 1e3, 2),
+                                     frac=round(alg_bytes / (cold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                     what=f"the first {args.steps} launches after {args.cold_idle:g} s idle, before "
+                                          f"the warmup (clock / power transient: profiles/r06_warp_burst.txt)")
+                                if cold_ms else None),
                     algorithmic_bytes_per_launch=int(alg_bytes),
                     copy_ceiling=dict(achieved=round(copy_gbs, 1), avg_launch_us=round(copy_ms * 1e3, 2),
                                       what="linear 3 B/px pass, 16 B/lane, non-temporal (k_stream3)"),

@@ -1544,9 +1544,19 @@ extern "C" int mdx_band_fit_warp_dev(mdx_ctx* c, int nrec, const mdx_band_cand* 
 }
 
 // Test hook: copy an internal LK v2 buffer to the host (0 = A sums, 1 = per-level trace).
+#if MDX_WARP_STAMP
+namespace mdx { hipError_t debug_warp_stamps(void* dst, size_t bytes); }
+#endif
 extern "C" int mdx_debug_copy(mdx_ctx* c, int which, void* dst, size_t bytes)
 {
     if (!c || !dst) return MDX_EINVAL;
+#if MDX_WARP_STAMP
+    if (which == 99) {   // diagnostic build: the warp's in-kernel clock stamps (scripts/warp_burst.py)
+        HIP_OR_RETURN(c, hipDeviceSynchronize());
+        HIP_OR_RETURN(c, debug_warp_stamps(dst, bytes));
+        return MDX_OK;
+    }
+#endif
     DevBuf& b = which == 0 ? c->Abuf : which == 1 ? c->dbg : which == 2 ? c->pyr1 : which == 3 ? c->pyr2
               : which == 4 ? c->der : c->cls;
     if (!b.p) return set_err(c, MDX_EINVAL, "debug buffer %d unavailable", which);

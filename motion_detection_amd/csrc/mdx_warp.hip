@@ -488,6 +488,26 @@ __device__ __noinline__ void stage_edge_chunks(const uint8_t* src, int pitch, in
     }
 }
 
+#ifndef MDX_WARP_STAMP
+#define MDX_WARP_STAMP 0
+#endif
+#if MDX_WARP_STAMP
+// Diagnostic build only (-DMDX_WARP_STAMP=1, scripts/warp_burst.py): per launch, 64 sampled workgroups'
+// thread 0 stamps s_memtime (shader clock) and s_memrealtime (100 MHz) at its start and end, so the
+// in-kernel clock of every launch of a burst is Δmemtime / Δmemrealtime x 100 MHz
+// (MI355X_MICROARCH.md DVFS item 6).  k_warp_prep counts the launches.
+constexpr int kStampLaunches = 1024, kStampSamples = 64;
+__device__ unsigned int g_warp_launch;
+__device__ unsigned long long g_warp_stamps[kStampLaunches * kStampSamples * 4];
+hipError_t debug_warp_stamps(void* dst, size_t bytes)
+{
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_warp_stamps), bytes < sizeof(g_warp_stamps) ? bytes : sizeof(g_warp_stamps));
+}
+#define WARP_DIFF_FN __device__ __forceinline__ void warp_diff_tile
+#else
+#define WARP_DIFF_FN __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_warp_diff
+#endif
+
 // Per-pair tables of the fixed-point path, made once per launch by k_warp_prep instead of once per
 // tile: B(x1) = floor(2^19 Wd fl(M*x1)) per axis and column of a block, and the bucket maps (for
 // column x1, A's fraction is bad iff it lies within -B(x1) - 3 .. -B(x1) + 1 mod 2^19; the buckets
@@ -512,6 +532,9 @@ __global__ __launch_bounds__(256) void k_warp_prep(const PairFit* __restrict__ f
                                                    WarpPrep* __restrict__ prep)
 {
     const int pair = blockIdx.y, tid = threadIdx.x;
+#if MDX_WARP_STAMP
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) g_warp_launch = g_warp_launch + 1;
+#endif
     const PairFit& f = fits[pair];
     if (f.fit_status != 0) return;
     double M[9];
@@ -549,7 +572,7 @@ __global__ __launch_bounds__(256) void k_warp_prep(const PairFit* __restrict__ f
 // on (x, y) only, so a band is exactly the full frame's rows.  The tile's footprint bounds and
 // the pair's fixed-point tables come from k_warp_prep, so the setup has one barrier: footprint
 // DMA, gray2 loads and the per-row-block table in flight together, then the row loop.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_warp_diff(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
+WARP_DIFF_FN(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
                                                    const uint8_t* __restrict__ g2, long long g2_stride, int g2_pitch,
                                                    int w, int h, int bw0, const PairFit* __restrict__ fits,
                                                    uint8_t* __restrict__ mask, long long mask_stride, int thresh,
@@ -740,6 +763,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
                      8 * g2_pitch, mrs, moff, 8 * w, tx0, ty0, tws0, M, x1b, mX, mY, mXs, mYs, bias);
     }
 }
+
+#if MDX_WARP_STAMP
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_warp_diff(
+    const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch, const uint8_t* __restrict__ g2,
+    long long g2_stride, int g2_pitch, int w, int h, int bw0, const PairFit* __restrict__ fits,
+    uint8_t* __restrict__ mask, long long mask_stride, int thresh, int vec_ok, int row0, int row1,
+    const TileInfo* __restrict__ tinfo, const WarpPrep* __restrict__ prep)
+{
+    const unsigned total = gridDim.x * gridDim.y * gridDim.z;
+    const unsigned bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const unsigned step = (total + kStampSamples - 1) / kStampSamples;
+    const bool stamp = threadIdx.x == 0 && bid % step == 0;
+    unsigned long long* st = g_warp_stamps + ((size_t)(g_warp_launch % kStampLaunches) * kStampSamples + bid / step) * 4;
+    if (stamp) {
+        st[0] = __builtin_amdgcn_s_memtime();
+        st[1] = __builtin_amdgcn_s_memrealtime();
+    }
+    warp_diff_tile(g1, g1_stride, g1_pitch, g2, g2_stride, g2_pitch, w, h, bw0, fits, mask, mask_stride, thresh,
+                   vec_ok, row0, row1, tinfo, prep);
+    if (stamp) {
+        st[2] = __builtin_amdgcn_s_memtime();
+        st[3] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+#endif
 
 size_t warp_scratch_bytes(int batch, int w, int rows)
 {
