@@ -44,6 +44,9 @@ Image to_rgb8(const Image& msg)
 MotionDetectionNode::MotionDetectionNode(const Params& p, int device, int max_w, int max_h, Publisher pub)
     : p_(p), pub_(std::move(pub))
 {
+    // the library must match the header this node was built against (ABI 4)
+    if (mdx_abi_version() != MDX_ABI_VERSION || mdx_params_size() != sizeof(mdx_params))
+        throw std::runtime_error("libmdx.so does not match include/mdx.h (ABI / mdx_params size)");
     mdx_params mp;
     mdx_default_params(&mp);
     mp.pixel_step = p_.pixel_step;
