@@ -61,7 +61,10 @@ struct mdx_ctx {
     int* tcnt_host = nullptr;                // pinned readback of the trajectory counts
     long long lk_fallback[3] = {0, 0, 0};
     int spin_max = kLkSpinDefault;           // MDX_LK_SPIN_MAX (debug: < 0 injects timeouts)
-    int lk_cap = 85;                         // MDX_LK_CAP: dataflow launch share of the resident waves (%)
+    // MDX_LK_CAP: dataflow launch share of the resident waves (%).  75: the aux stream's next-level
+    // class planes and A sums pace the level hand-offs (round 6, profiles/r06_ab_lk_w5_cap.txt: 60 -3%,
+    // 70 / 80 / 85 within 1%, 75 best and steadiest, 95 -1.2%)
+    int lk_cap = 75;
     // pipelined calls alternate the LK stream parity (MDX_LK_XCALL=1): the next call's first level
     // then need not queue behind this call's fit / warp.  Measured +0.5% (within noise; the chip is
     // already saturated by the aux work in that gap), and it moves the LK stage events, so it is off
