@@ -184,10 +184,14 @@ typedef __attribute__((address_space(3))) const d2v lds_d2;
 
 // raw buffer descriptor over [base, base + bytes): out-of-range loads return 0 and stores are
 // dropped, which is how lanes past the right edge and rows past the band go quiet.
+// (The clamp is done on the 32-bit halves: a 64-bit signed min has no scalar instruction, and
+// the compiler put it on the VALU.)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, long long bytes)
 {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
-                                             (int)min(bytes, (long long)0x7fffffff), 0x00020000);
+    uint32_t hi = (uint32_t)((unsigned long long)bytes >> 32), lo = (uint32_t)bytes;
+    asm("" : "+s"(hi), "+s"(lo));   // keep the halves apart (else it is re-fused into a VALU compare)
+    const int n = (int)min(lo | (0u - (uint32_t)(hi != 0u)), 0x7fffffffu);   // bytes >= 0
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, n, 0x00020000);
 }
 
 // Fast-path rows of one lane: 4 columns x 8 rows (tile rows r0 + 8i).  xyp points at this lane's
@@ -508,6 +512,20 @@ hipError_t debug_warp_stamps(void* dst, size_t bytes)
 #define WARP_DIFF_FN __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_warp_diff
 #endif
 
+// n / d for uniform n, d < 2^31 with m = udiv_magic_of(d) = floor(2^32 / d) (d >= 2; m = 0 for d = 1):
+// the estimate mulhi(n, m) is q or q - 1, one correction makes it exact; all scalar instructions
+static inline uint32_t udiv_magic_of(uint32_t d)
+{
+    return d > 1 ? (uint32_t)(0x100000000ull / d) : 0u;
+}
+__device__ __forceinline__ uint32_t udiv_magic(uint32_t n, uint32_t d, uint32_t m)
+{
+    if (d == 1) return n;
+    uint32_t q = __umulhi(n, m);
+    if (n - q * d >= d) q++;
+    return q;
+}
+
 // Per-pair tables of the fixed-point path, made once per launch by k_warp_prep instead of once per
 // tile: B(x1) = floor(2^19 Wd fl(M*x1)) per axis and column of a block, and the bucket maps (for
 // column x1, A's fraction is bad iff it lies within -B(x1) - 3 .. -B(x1) + 1 mod 2^19; the buckets
@@ -577,7 +595,7 @@ WARP_DIFF_FN(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
                                                    int w, int h, int bw0, const PairFit* __restrict__ fits,
                                                    uint8_t* __restrict__ mask, long long mask_stride, int thresh,
                                                    int vec_ok, int row0, int row1, const TileInfo* __restrict__ tinfo,
-                                                   const WarpPrep* __restrict__ prep)
+                                                   const WarpPrep* __restrict__ prep, uint32_t mt, uint32_t mx)
 {
     __shared__ __attribute__((aligned(16))) uint32_t s_tab[64];             // weight table (FP64 rows)
     __shared__ __attribute__((aligned(16))) double s_xy[kTH][2][2];         // (X0, Y0) per row, block
@@ -596,8 +614,9 @@ WARP_DIFF_FN(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
         const int total = nbx * nby * gridDim.z, xcd = bid & 7, q8 = total >> 3, r8 = total & 7;
         bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     }
-    const int pair = bid / (nbx * nby), tile = bid - pair * (nbx * nby);
-    const int tx_ = tile % nbx, ty_ = tile / nbx;
+    // the divisions by uniform values with host magic numbers: scalar multiplies, no VALU
+    const int pair = (int)udiv_magic((uint32_t)bid, (uint32_t)(nbx * nby), mt), tile = bid - pair * (nbx * nby);
+    const int ty_ = (int)udiv_magic((uint32_t)tile, (uint32_t)nbx, mx), tx_ = tile - ty_ * nbx;
     // The tile's scalar operands (the pair's fit, the tile's TileInfo) in ONE round trip: left to
     // itself the compiler sinks each scalar load into the branch that first uses it, and the DMA
     // then waits behind five dependent scalar-load latencies (kernel arguments, fit status, more
@@ -671,12 +690,22 @@ WARP_DIFF_FN(const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch,
     const bool inner = ch < nch && sx >= 0 && sx + 16 <= w;
     {
         const __amdgpu_buffer_rsrc_t srs = buf_rsrc(src, (long long)h * g1_pitch);
+        // A group of 4 staged rows wholly inside the image and the footprint (all but the edge
+        // tiles' first / last groups) needs no per-lane test: the lane's offset within the group is
+        // loop-invariant and the group's row start is the scalar offset (0 VALU per DMA instead of 6)
+        const uint32_t voff = inner ? (uint32_t)((lane >> 4) * g1_pitch + sx) : 0x80000000u;
         for (int q = wave; 4 * q < t.sh; q += 4) {
-            const int r = 4 * q + (lane >> 4);
-            const int sy = t.sya + r;
-            const uint32_t off = (inner && r < t.sh && (unsigned)sy < (unsigned)h) ? (uint32_t)(sy * g1_pitch + sx)
-                                                                                  : 0x80000000u;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, (lds_ptr)&s_src[4 * q * kSP], 16, (int)off, 0, 0, 0);
+            const int y4 = t.sya + 4 * q;
+            if (y4 >= 0 && y4 + 4 <= h && 4 * q + 4 <= t.sh) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, (lds_ptr)&s_src[4 * q * kSP], 16, (int)voff,
+                                                         y4 * g1_pitch, 0, 0);
+            } else {
+                const int r = 4 * q + (lane >> 4);
+                const int sy = t.sya + r;
+                const uint32_t off = (inner && r < t.sh && (unsigned)sy < (unsigned)h)
+                                         ? (uint32_t)(sy * g1_pitch + sx) : 0x80000000u;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, (lds_ptr)&s_src[4 * q * kSP], 16, (int)off, 0, 0, 0);
+            }
         }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -769,7 +798,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     const uint8_t* __restrict__ g1, long long g1_stride, int g1_pitch, const uint8_t* __restrict__ g2,
     long long g2_stride, int g2_pitch, int w, int h, int bw0, const PairFit* __restrict__ fits,
     uint8_t* __restrict__ mask, long long mask_stride, int thresh, int vec_ok, int row0, int row1,
-    const TileInfo* __restrict__ tinfo, const WarpPrep* __restrict__ prep)
+    const TileInfo* __restrict__ tinfo, const WarpPrep* __restrict__ prep, uint32_t mt, uint32_t mx)
 {
     const unsigned total = gridDim.x * gridDim.y * gridDim.z;
     const unsigned bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
@@ -781,7 +810,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         st[1] = __builtin_amdgcn_s_memrealtime();
     }
     warp_diff_tile(g1, g1_stride, g1_pitch, g2, g2_stride, g2_pitch, w, h, bw0, fits, mask, mask_stride, thresh,
-                   vec_ok, row0, row1, tinfo, prep);
+                   vec_ok, row0, row1, tinfo, prep, mt, mx);
     if (stamp) {
         st[2] = __builtin_amdgcn_s_memtime();
         st[3] = __builtin_amdgcn_s_memrealtime();
@@ -815,7 +844,8 @@ hipError_t launch_warp_diff(hipStream_t s, int batch, const uint8_t* g1, long lo
     hipLaunchKernelGGL(k_warp_prep, dim3(1 + (ntiles + 31) / 32, batch), dim3(256), 0, s, fits, w, row0, row1,
                        (int)grid.x, (int)grid.y, tinfo, prep);
     hipLaunchKernelGGL(k_warp_diff, grid, dim3(256), 0, s, g1, g1_stride, g1_pitch, g2, g2_stride, g2_pitch, w, h, bw0,
-                       fits, mask, mask_stride, thresh, vec_ok, row0, row1, tinfo, prep);
+                       fits, mask, mask_stride, thresh, vec_ok, row0, row1, tinfo, prep, udiv_magic_of((uint32_t)ntiles),
+                       udiv_magic_of(grid.x));
     return hipGetLastError();
 }
 
