@@ -64,6 +64,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, lon
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
                                              (int)min(bytes, (long long)0x7fffffff), 0x00020000);
 }
+// the same for wave-uniform inputs and a size the host keeps below 2 GB: the inputs pass through
+// readfirstlane so that the compiler can prove the descriptor uniform (scalar instructions, no
+// waterfall loop around the memory op; cdna_hip_programming.md T8)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc32(const void* base, uint32_t bytes)
+{
+    const unsigned long long b = (unsigned long long)(uintptr_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    void* p = (void*)(uintptr_t)(((unsigned long long)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
 
 // residue-class tables: [level][axis][128]
 __device__ __forceinline__ int class_of(const int16_t* cmap, int level, int axis, int res)
@@ -774,10 +784,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
     const Level L = a.g.lv[level];
     // buffer addressing: descriptors over the range's class slabs and next-frame pyramids (the
     // host keeps them below 2 GB), 32-bit lane offsets
-    const __amdgpu_buffer_rsrc_t crs = buf_rsrc(cls + (long long)p0 * a.plan.bytes_per_pair, np * a.plan.bytes_per_pair);
+    const uint8_t* const cls_base = cls + (long long)p0 * a.plan.bytes_per_pair;
+    const uint32_t cls_bytes = (uint32_t)(np * a.plan.bytes_per_pair);
     const uint32_t rowb = (uint32_t)C.PW * 8;
     const int pitch = L.pitch;
-    const __amdgpu_buffer_rsrc_t jrs = buf_rsrc(a.pyr2 + (long long)p0 * a.g.img_bytes, np * a.g.img_bytes);
+    const uint8_t* const j_base = a.pyr2 + (long long)p0 * a.g.img_bytes;
+    const uint32_t j_bytes = (uint32_t)(np * a.g.img_bytes);
     const uint32_t jbase = (uint32_t)(L.img_off + L.core());
     const float scale = (float)(1. / (1 << level));
 
@@ -975,19 +987,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
             else if constexpr (bb == 1) return dJ1;
             else return dJ2;
         };
-        auto dma_union = [&](auto bc) {
+        // window row yr of the union / J images: the per-lane offsets stay fixed and the row
+        // advance moves the descriptor's base (and shrinks its size by as much, so the range check
+        // keeps the same end): scalar work instead of a VALU add per piece and row
+        auto dma_union = [&](auto bc, int yr) {
             uint32_t* U = ubuf(bc);
+            const uint32_t adv = (uint32_t)yr * rowb;
+            const __amdgpu_buffer_rsrc_t r = buf_rsrc32(cls_base + adv, cls_bytes - adv);
 #pragma unroll
             for (int c = 0; c < ND; c++) {
                 if (c < ND - 1 || 1024 * c + 16 * lane < Sh::BYTES)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(crs, (lds_ptr)(U + 256 * c), 16, (int)uoff[c], 0, 0, 0);
-                uoff[c] += rowb;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr)(U + 256 * c), 16, (int)uoff[c], 0, 0, 0);
             }
         };
-        auto dma_j = [&](auto bc) {
+        auto dma_j = [&](auto bc, int yr) {
             // the quad's taps span 44 bytes: lanes 0-2 carry them, lane 3 stays idle
-            if (k < 3) __builtin_amdgcn_raw_ptr_buffer_load_lds(jrs, (lds_ptr)jbuf(bc), 16, (int)joff, 0, 0, 0);
-            joff += (uint32_t)pitch;
+            const uint32_t adv = (uint32_t)(yr * pitch);
+            const __amdgpu_buffer_rsrc_t r = buf_rsrc32(j_base + adv, j_bytes - adv);
+            if (k < 3) __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr)jbuf(bc), 16, (int)joff, 0, 0, 0);
         };
         const int jl = (lane >> 2) * 16, el = 2 * (slot * UW + q.off + k);
         auto read_j = [&](auto bc, uint32_t (&rj)[11]) {
@@ -1004,12 +1021,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
         using I2 = std::integral_constant<int, 2>;
         // taps of the current window row (pa) are the previous row's lower taps (pb)
         s2 pa[10], pb[10];
-        dma_union(I0{});
-        dma_j(I0{});
-        dma_j(I1{});
+        dma_union(I0{}, 0);
+        dma_j(I0{}, 0);
+        dma_j(I1{}, 1);
         if constexpr (D == 2) {
-            dma_union(I1{});
-            dma_j(I2{});
+            dma_union(I1{}, 1);
+            dma_j(I2{}, 2);
         }
         lk_vmcnt<(D - 1) * (ND + 1)>();
         {
@@ -1026,8 +1043,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kLkIterWaves
             constexpr int R = decltype(Rc)::value, W = decltype(Wc)::value;
             if (y) lk_vmcnt<W>();
             auto fetch = [&]() {
-                if (y + D < kWin) dma_union(std::integral_constant<int, (R + D) % NB>{});
-                if (y + D + 1 <= kWin) dma_j(std::integral_constant<int, (R + D + 1) % NB>{});
+                if (y + D < kWin) dma_union(std::integral_constant<int, (R + D) % NB>{}, y + D);
+                if (y + D + 1 <= kWin) dma_j(std::integral_constant<int, (R + D + 1) % NB>{}, y + D + 1);
                 __builtin_amdgcn_sched_barrier(0);
             };
 #if !MDX_LK_RFIRST
