@@ -376,14 +376,15 @@ __device__ __forceinline__ void warp_rows_fx(lds_u4* fxp, lds_d2* xyp, uint32_t 
 // Projective rows.  The reference's X = cvRound(fl(fl(X0 + fl(M0*x1)) * fl(32 / fl(W0 + fl(M6*x1))))) is
 // taken in two steps.  First an estimate, in warp_rows_fx's fixed-point layout relative to the
 // staged origin (U = [ staged column (8 bits) | fx (5 bits) | fraction (19 bits) ], U ~ 2^19 (X' + 1/2)):
-// r ~ 2^24 / W from v_rcp_f64 and one cubic Newton step (rcp's relative error e -> e^3, about
-// 2^-69, plus the step's own roundings, ~2^-52), then U = RN(ax * r + 2^18 - 2^24 sxa), one FMA
-// per axis.  The estimate's operands need not be the reference's roundings: ax and W / 2^24 of
+// r ~ 2^24 / W from v_rcp_f64 and one quadratic Newton step (rcp's relative error e -> e^2:
+// measured at most 2^-24.4 -> 2^-48.7 over 16 M values, scripts/micro/rcp64_acc.hip; round 5 used a
+// cubic step), then U = RN(ax * r + 2^18 - 2^24 sxa), one FMA per axis.  The estimate's operands need not be the reference's roundings: ax and W / 2^24 of
 // column x1b + k come from the lane's column x1b by k more FMAs (ax = fl(M0 * k + fl(X0 + M0 * x1b))),
 // so no per-column table is held in registers.  tile_info keeps projective fast tiles at |X|, |Y| <
 // 2^24 (1/32 px units) and |W| >= 64 |M6| at the corners (no cancellation in W0 + M6 * x1), so the
-// estimate and the reference each stay within 2^24 * 2^19 * 2^-49 = 1/64 unit of 2^-19 of the exact
-// quotient: whenever U's fraction is at least kPjGuard units from the boundary (0), floor(U / 2^19)
+// estimate stays within 2^24 * 2^19 * 2^-47 = 1/16 unit of 2^-19 of the exact quotient and the
+// reference within 2^-9 unit (an rcp 16x less accurate than measured would still give < 8 units):
+// whenever U's fraction is at least kPjGuard units from the boundary (0), floor(U / 2^19)
 // is the reference's X' and not a tie.  The other pixels (64 of every 2^19 fractions per axis) take
 // the exact form: W, the correctly rounded 32/W (div32) and the rounded product.  Then the taps,
 // weights and threshold are warp_rows_fx's.
@@ -424,7 +425,7 @@ __device__ __forceinline__ void warp_rows_pj(lds_d2* xyp, lds_d2* wpp, uint32_t 
             const double Ws = k ? __builtin_fma(M6s, kd, ws0) : ws0;   // ~ W / 2^24
             const double r0 = __builtin_amdgcn_rcp(Ws);
             const double e = __builtin_fma(-Ws, r0, 1.0);
-            const double r = __builtin_fma(r0, __builtin_fma(e, e, e), r0);
+            const double r = __builtin_fma(r0, e, r0);
             ux[k] = (uint32_t)__double2loint(__builtin_fma(ax, r, mXs));
             uy[k] = (uint32_t)__double2loint(__builtin_fma(ay, r, mYs));
             fmin = min(fmin, min((ux[k] + kPjGuard) & 0x7ffffu, (uy[k] + kPjGuard) & 0x7ffffu));
