@@ -379,9 +379,9 @@ __device__ __forceinline__ void warp_rows_fx(lds_u4* fxp, lds_d2* xyp, uint32_t 
 // r ~ 2^24 / W from v_rcp_f64 and one quadratic Newton step (rcp's relative error e -> e^2:
 // measured at most 2^-24.4 -> 2^-48.7 over 16 M values, scripts/micro/rcp64_acc.hip; round 5 used a
 // cubic step), one reciprocal per four pixels (of the product of their W), then
-// U = RN(ax * r + 2^18 - 2^24 sxa), one FMA per axis.  The estimate's operands need not be the reference's roundings: ax and W / 2^24 of
-// column x1b + k come from the lane's column x1b by k more FMAs (ax = fl(M0 * k + fl(X0 + M0 * x1b))),
-// so no per-column table is held in registers.  tile_info keeps projective fast tiles at |X|, |Y| <
+// U = RN(ax * r + 2^18 - 2^24 sxa), one FMA per axis.  The estimate's operands need not be the
+// reference's roundings: ax and W / 2^24 of column x1b + k come from the lane's column x1b by k
+// adds of the per-column steps, so no per-column table is held in registers.  tile_info keeps projective fast tiles at |X|, |Y| <
 // 2^24 (1/32 px units) and |W| >= 64 |M6| at the corners (no cancellation in W0 + M6 * x1), so the
 // estimate stays within 2^24 * 2^19 * 2^-47 = 1/16 unit of 2^-19 of the exact quotient and the
 // reference within 2^-9 unit (an rcp 16x less accurate than measured would still give < 8 units):
@@ -417,29 +417,36 @@ __device__ __forceinline__ void warp_rows_pj(lds_d2* xyp, lds_d2* wpp, uint32_t 
         const d2v wv = wpp[16 * ri];                      // (W0, W0 / 2^24)
         const double ax0 = xy.x + tx0, ay0 = xy.y + ty0, ws0 = wv.y + tws0;
         uint32_t ux[4], uy[4];
-        uint32_t fmin = 0xffffffffu;                      // the smallest guard-shifted fraction
+        uint32_t fmin = 0xffffffffu;                      // the smallest guard-shifted fraction (x 2^13)
         // the four reciprocals from ONE v_rcp_f64 (a transcendental, several times an FMA's issue
         // cost) of the product of the four W: 1/W_k = (product of the other three) / P.  Six more
         // roundings of 2^-53 keep r within 2^-48 of 2^24 / W (the guard needs 2^-40, see above);
         // |W| in [2^-100, 2^100] (tile_info) keeps P inside FP64's range
+        // column x1b + k by k adds of the per-column steps (the estimate needs accuracy, not the
+        // reference's roundings: 3 more roundings of 2^-53), the steps are scalar operands
         double Ws[4];
+        Ws[0] = ws0;                                      // ~ W / 2^24
 #pragma unroll
-        for (int k = 0; k < 4; k++) Ws[k] = k ? __builtin_fma(M6s, (double)k, ws0) : ws0;   // ~ W / 2^24
+        for (int k = 1; k < 4; k++) Ws[k] = Ws[k - 1] + M6s;
         const double P01 = Ws[0] * Ws[1], P23 = Ws[2] * Ws[3], P = P01 * P23;
         const double R0 = __builtin_amdgcn_rcp(P);
         const double R = __builtin_fma(R0, __builtin_fma(-P, R0, 1.0), R0);
         const double R01 = R * P23, R23 = R * P01;       // 1 / P01, 1 / P23
         const double rk[4] = {Ws[1] * R01, Ws[0] * R01, Ws[3] * R23, Ws[2] * R23};
+        double ax = ax0, ay = ay0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const double kd = (double)k;
-            const double ax = k ? __builtin_fma(M[0], kd, ax0) : ax0;
-            const double ay = k ? __builtin_fma(M[3], kd, ay0) : ay0;
+            if (k) {
+                ax = ax + M[0];
+                ay = ay + M[3];
+            }
             ux[k] = (uint32_t)__double2loint(__builtin_fma(ax, rk[k], mXs));
             uy[k] = (uint32_t)__double2loint(__builtin_fma(ay, rk[k], mYs));
-            fmin = min(fmin, min((ux[k] + kPjGuard) & 0x7ffffu, (uy[k] + kPjGuard) & 0x7ffffu));
+            // ((u + G) & 0x7ffff) < 2G  <=>  (u << 13) + (G << 13) < 2G << 13 (mod 2^32): one
+            // v_lshl_add_u32 per value instead of an add and an and
+            fmin = min(fmin, min((ux[k] << 13) + (kPjGuard << 13), (uy[k] << 13) + (kPjGuard << 13)));
         }
-        if (fmin < 2 * kPjGuard) {
+        if (fmin < (2 * kPjGuard) << 13) {
             // within the guard of a rounding boundary (or on a tie): the reference's expression
 #pragma unroll
             for (int k = 0; k < 4; k++) {
