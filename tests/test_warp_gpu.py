@@ -123,6 +123,30 @@ def test_warp_4k_projective(mdx, wctx, oracle):
          [_H("projective", w, h, Ht), _H("proj_near_tie", w, h, Ht)], 190)
 
 
+def test_warp_projective_random(mdx, wctx, oracle):
+    """Random projective H across the projective fast path's range (round 6: one v_rcp_f64 per four
+    pixels of the product of their W, one quadratic Newton step, the shift-add boundary test):
+    perspective terms from 1e-7 to 4e-4 per pixel, rotations, anisotropic scales and translations
+    with 1/64-px parts, every mask byte against the oracle.  The first eight stay mild (|angle| <=
+    1 deg, scales 0.97-1.03, perspective <= 5e-5: W within ~10% over the frame), so nearly every
+    tile's footprint fits the staging buffer and takes the projective fast path; the last four are
+    strong (W varying by up to ~1.5x, a horizon in some), where tiles also fall back."""
+    w, h = 1920, 1080
+    rng = np.random.default_rng(20261018)
+    g1, g2, Hs = [], [], []
+    for i in range(12):
+        a, b, _ = mdx.synth_pair(900 + i, w, h, 1)
+        g1.append(a); g2.append(b)
+        mild = i < 8
+        ang = math.radians(rng.uniform(-1.0, 1.0) if mild else rng.uniform(-8.0, 8.0))
+        sx, sy = rng.uniform(0.97, 1.03, 2) if mild else rng.uniform(0.8, 1.25, 2)
+        p6, p7 = (rng.choice([-1.0, 1.0], 2) * 10.0 ** rng.uniform(-7.0, -4.3 if mild else -3.4, 2))
+        tx, ty = rng.uniform(-30, 30, 2) + rng.integers(0, 64, 2) / 64.0
+        Hs.append(np.array([[sx * math.cos(ang), -sy * math.sin(ang), tx],
+                            [sx * math.sin(ang), sy * math.cos(ang), ty], [p6, p7, 1.0]]))
+    _run(mdx, wctx, oracle, np.stack(g1), np.stack(g2), Hs, 190)
+
+
 def test_div32_is_ieee_division(mdx, wctx):
     """The projective fast path's 32 / W (mdx_warp.hip div32: the IEEE division sequence without its
     range-scaling steps) equals correctly rounded IEEE division bit for bit over its range
