@@ -482,6 +482,14 @@ __device__ __forceinline__ int sdot2_sacc(s2k a, s2k b, int c)
 constexpr int kChainSpinMax = 1 << 19;   // ~0.1 s of s_sleep(8) polls: a lost hand-off gives wrong
                                          // results, never a hung launch
 
+// four points per wave: each lane's 20 elements of a chunk as a block of 4 rows x 5 columns (1,
+// round 6) or as 20 columns of one row (0).  The block shares tap rows between its rows: 5 row
+// loads and 75 pair-building v_perm per chunk (I taps, Ix and Iy pairs) instead of 2 x 2 loads and
+// 120, and its J rows for the next chunk are loaded while the current one is summed (ring callback
+// 2.37 against 2.49 ms, profiles/r06_ab_traj_blk.txt)
+#ifndef MDX_TRAJ_BLK
+#define MDX_TRAJ_BLK 1
+#endif
 // two points per wave: 144 VGPRs, 3 waves per SIMD (MDX_LK32_WPE=4 squeezes 128 with spills)
 #ifndef MDX_LK32_WPE
 #define MDX_LK32_WPE 1
@@ -516,10 +524,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
     // columns of one row per 8-row chunk (row s >> 3, columns 5 (s & 7) .. +4), so its taps of a
     // chunk are two 12-B row loads (J: v_perm + v_dot2 tap pairs) instead of 4 byte loads per element
     static_assert(RUN == 0 || EC == RUN, "row runs of RUN columns");
+    constexpr bool BLK = MDX_TRAJ_BLK && LPP == 16;   // lane s: rows 4 (s / 8) .. +3, columns 5 (s % 8) .. +4
     int woff[EC], ex[EC], ey[EC];
 #pragma unroll
     for (int i = 0; i < EC; i++) {
-        const int e = RUN ? (s / (WIN / RUN)) * WIN + RUN * (s % (WIN / RUN)) + i : s + LPP * i;
+        const int e = BLK ? (4 * (s / 8) + i / 5) * WIN + 5 * (s % 8) + i % 5
+                    : RUN ? (s / (WIN / RUN)) * WIN + RUN * (s % (WIN / RUN)) + i : s + LPP * i;
         ey[i] = e / WIN;
         ex[i] = e % WIN;
         woff[i] = (ex[i] & 3) * STRIDE + ey[i] * 10 + (ex[i] >> 2);
@@ -636,7 +646,50 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
         float acc = 0.f;
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
-            if (ok) {
+            if (ok && BLK) {
+                // 4 x 5 block: rows a = 0 .. 4 of the block (4 element rows + the lower tap row),
+                // each 6 I bytes and 6 derivative words; row a's tap / Ix / Iy pairs serve element row
+                // a as its upper taps and element row a - 1 as its lower ones
+                const int o = ibase + c * R * pitch + toff[0];
+                const s2k W0 = {(short)w00, (short)w01}, W1 = {(short)w10, (short)w11};
+                s2k pu[5], xu[5], yu[5];
+#pragma unroll
+                for (int ar = 0; ar <= 4; ar++) {
+                    uint32_t lo, hi;
+                    row8(Ib + o + ar * pitch, lo, hi);
+                    const uint32_t* q = Db + o + ar * pitch;
+                    const u4a4k v = *reinterpret_cast<const u4a4k*>(q);
+                    const u2a4k w2 = *reinterpret_cast<const u2a4k*>(q + 4);
+                    const uint32_t d[6] = {v.x, v.y, v.z, v.w, w2.x, w2.y};
+                    s2k pl[5], xl[5], yl[5];
+#pragma unroll
+                    for (int b = 0; b < 5; b++) {
+                        const unsigned sel = 0x0c000c00u | (unsigned)b | ((unsigned)(b + 1) << 16);
+                        pl[b] = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(hi, lo, sel));
+                        xl[b] = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(d[b + 1], d[b], 0x05040100u));
+                        yl[b] = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(d[b + 1], d[b], 0x07060302u));
+                    }
+                    if (ar > 0) {
+#pragma unroll
+                        for (int b = 0; b < 5; b++) {
+                            const int i = 5 * (ar - 1) + b;
+                            const int ival = __builtin_amdgcn_sdot2(pu[b], W0, sdot2_sacc(pl[b], W1, 256), false) >> 9;
+                            const int ixv = __builtin_amdgcn_sdot2(xu[b], W0, sdot2_sacc(xl[b], W1, 8192), false) >> 14;
+                            const int iyv = __builtin_amdgcn_sdot2(yu[b], W0, sdot2_sacc(yl[b], W1, 8192), false) >> 14;
+                            const int k = c * EC + i;
+                            sd[k] = ((uint32_t)ixv & 0xffffu) | ((uint32_t)iyv << 16);
+                            if (k & 1) si[k >> 1] = (si[k >> 1] & 0xffffu) | ((uint32_t)ival << 16);
+                            else si[k >> 1] = (uint32_t)ival;
+                            float* wp = ch + woff[i];
+                            wp[0] = (float)__mul24(ixv, ixv);
+                            wp[4 * STRIDE] = (float)__mul24(ixv, iyv);
+                            wp[8 * STRIDE] = (float)__mul24(iyv, iyv);
+                        }
+                    }
+#pragma unroll
+                    for (int b = 0; b < 5; b++) { pu[b] = pl[b]; xu[b] = xl[b]; yu[b] = yl[b]; }
+                }
+            } else if (ok) {
                 // LPP 64: the run's I bytes and derivative words of both tap rows, vector loads
                 uint64_t r0 = 0, r1 = 0;
                 uint32_t dr0[RUN >= 10 ? RUN + 1 : 6] = {}, dr1[RUN >= 10 ? RUN + 1 : 6] = {};
@@ -798,9 +851,56 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
                 }
             }
             float bacc = 0.f;
+            // BLK: the block's five J rows of chunk c + 1 are loaded while chunk c is summed (two waves
+            // per SIMD hide little of a global load's latency); pitch is a multiple of 64, so one
+            // realignment shift serves every row and chunk
+            u3a4k jr[BLK ? 5 : 1] = {};
+            uint32_t jsh = 0;
+            const uint8_t* jb0 = nullptr;
+            if (BLK && act) {
+                const uintptr_t u = reinterpret_cast<uintptr_t>(Jb + (jbase + toff[0]));
+                jsh = (uint32_t)(u & 3);
+                jb0 = reinterpret_cast<const uint8_t*>(u & ~(uintptr_t)3);
+#pragma unroll
+                for (int ar = 0; ar < (BLK ? 5 : 1); ar++) jr[ar] = *reinterpret_cast<const u3a4k*>(jb0 + ar * pitch);
+            }
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
-                if (act) {
+                if (act && BLK) {
+                    const s2k W0 = {(short)v00, (short)v01}, W1 = {(short)v10, (short)v11};
+                    s2k pu[5];
+#pragma unroll
+                    for (int ar = 0; ar <= 4; ar++) {
+                        const uint32_t lo = __builtin_amdgcn_alignbyte(jr[BLK ? ar : 0].y, jr[BLK ? ar : 0].x, jsh);
+                        const uint32_t hi = __builtin_amdgcn_alignbyte(jr[BLK ? ar : 0].z, jr[BLK ? ar : 0].y, jsh);
+                        s2k pl[5];
+#pragma unroll
+                        for (int b = 0; b < 5; b++) {
+                            const unsigned sel = 0x0c000c00u | (unsigned)b | ((unsigned)(b + 1) << 16);
+                            pl[b] = __builtin_bit_cast(s2k, __builtin_amdgcn_perm(hi, lo, sel));
+                        }
+                        if (ar > 0) {
+#pragma unroll
+                            for (int b = 0; b < 5; b++) {
+                                const int i = 5 * (ar - 1) + b;
+                                const int jv = __builtin_amdgcn_sdot2(pu[b], W0, sdot2_sacc(pl[b], W1, 256), false) >> 9;
+                                const int k = c * EC + i;
+                                const int iv = (k & 1) ? (int)(si[k >> 1] >> 16) : (int)(si[k >> 1] & 0xffffu);
+                                const int diff = jv - iv;
+                                const uint32_t dv = sd[k];
+                                float* wp = ch + woff[i];
+                                wp[0] = (float)__mul24(diff, (int)(int16_t)dv);
+                                wp[4 * STRIDE] = (float)__mul24(diff, (int)dv >> 16);
+                            }
+                        }
+#pragma unroll
+                        for (int b = 0; b < 5; b++) pu[b] = pl[b];
+                    }
+                    if (c + 1 < NCH)
+#pragma unroll
+                        for (int ar = 0; ar < (BLK ? 5 : 1); ar++)
+                            jr[ar] = *reinterpret_cast<const u3a4k*>(jb0 + ((c + 1) * R + ar) * pitch);
+                } else if (act) {
                     uint32_t j0l = 0, j0h = 0, j1l = 0, j1h = 0;
                     uint32_t j0w[RW > 0 ? RW : 1] = {}, j1w[RW > 0 ? RW : 1] = {};
                     if constexpr (LPP == 16) {
