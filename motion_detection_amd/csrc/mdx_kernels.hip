@@ -41,6 +41,19 @@ __device__ __forceinline__ int r101(int p, int len)
 struct __attribute__((aligned(4))) u4a4k { uint32_t x, y, z, w; };
 struct __attribute__((aligned(4))) u3a4k { uint32_t x, y, z; };
 struct __attribute__((aligned(4))) u2a4k { uint32_t x, y; };
+// a load from a global address held as an integer: through an address-space-1 pointer, so that it is
+// a global_load (vmcnt only).  Through a generic pointer it is a flat_load, which also counts in
+// lgkmcnt: every LDS wait would then wait for it, and a load issued ahead of use would be waited
+// for at the next LDS access.
+template <typename T>
+__device__ __forceinline__ T gload(uintptr_t a)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *reinterpret_cast<const __attribute__((address_space(1))) T*>(a);
+#else
+    return *reinterpret_cast<const T*>(a);   // the host pass only type-checks device code
+#endif
+}
 
 __device__ __forceinline__ int gray_of(const uint8_t* s, int fmt)
 {
@@ -537,7 +550,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
     // 12 bytes of a row from byte address p, realigned: (lo, hi) = bytes p .. p+7
     auto row8 = [](const uint8_t* p, uint32_t& lo, uint32_t& hi) {
         const uintptr_t u = reinterpret_cast<uintptr_t>(p);
-        const u3a4k v = *reinterpret_cast<const u3a4k*>(u & ~(uintptr_t)3);
+        const u3a4k v = gload<u3a4k>(u & ~(uintptr_t)3);
         const uint32_t o = (uint32_t)(u & 3);
         lo = __builtin_amdgcn_alignbyte(v.y, v.x, o);
         hi = __builtin_amdgcn_alignbyte(v.z, v.y, o);
@@ -545,7 +558,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
     // 16 bytes of a row from byte address p, realigned: w[0..2] = bytes p .. p+11 (runs of 10)
     auto row12 = [](const uint8_t* p, uint32_t (&w)[3]) {
         const uintptr_t u = reinterpret_cast<uintptr_t>(p);
-        const u4a4k v = *reinterpret_cast<const u4a4k*>(u & ~(uintptr_t)3);
+        const u4a4k v = gload<u4a4k>(u & ~(uintptr_t)3);
         const uint32_t o = (uint32_t)(u & 3);
         w[0] = __builtin_amdgcn_alignbyte(v.y, v.x, o);
         w[1] = __builtin_amdgcn_alignbyte(v.z, v.y, o);
@@ -554,8 +567,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
     // 28 bytes of a row from byte address p, realigned: w[0..5] = bytes p .. p+23 (runs of 20)
     auto row24 = [](const uint8_t* p, uint32_t (&w)[6]) {
         const uintptr_t u = reinterpret_cast<uintptr_t>(p);
-        const u4a4k v = *reinterpret_cast<const u4a4k*>(u & ~(uintptr_t)3);
-        const u3a4k x = *reinterpret_cast<const u3a4k*>((u & ~(uintptr_t)3) + 16);
+        const u4a4k v = gload<u4a4k>(u & ~(uintptr_t)3);
+        const u3a4k x = gload<u3a4k>((u & ~(uintptr_t)3) + 16);
         const uint32_t o = (uint32_t)(u & 3);
         w[0] = __builtin_amdgcn_alignbyte(v.y, v.x, o);
         w[1] = __builtin_amdgcn_alignbyte(v.z, v.y, o);
@@ -644,6 +657,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
 
         // ---- window extraction + A sums (chains q*4+k, q: 0 A11, 1 A12, 2 A22)
         float acc = 0.f;
+        u4a4k dpa[BLK ? 5 : 1] = {};
+        u2a4k dpb[BLK ? 5 : 1] = {};
+        if (BLK && ok)
+#pragma unroll
+            for (int ar = 0; ar < (BLK ? 5 : 1); ar++) {
+                const uint32_t* q = Db + (ibase + toff[0]) + ar * pitch;
+                dpa[ar] = *reinterpret_cast<const u4a4k*>(q);
+                dpb[ar] = *reinterpret_cast<const u2a4k*>(q + 4);
+            }
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             if (ok && BLK) {
@@ -657,9 +679,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
                 for (int ar = 0; ar <= 4; ar++) {
                     uint32_t lo, hi;
                     row8(Ib + o + ar * pitch, lo, hi);
-                    const uint32_t* q = Db + o + ar * pitch;
-                    const u4a4k v = *reinterpret_cast<const u4a4k*>(q);
-                    const u2a4k w2 = *reinterpret_cast<const u2a4k*>(q + 4);
+                    const u4a4k v = dpa[BLK ? ar : 0];
+                    const u2a4k w2 = dpb[BLK ? ar : 0];
                     const uint32_t d[6] = {v.x, v.y, v.z, v.w, w2.x, w2.y};
                     s2k pl[5], xl[5], yl[5];
 #pragma unroll
@@ -689,6 +710,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
 #pragma unroll
                     for (int b = 0; b < 5; b++) { pu[b] = pl[b]; xu[b] = xl[b]; yu[b] = yl[b]; }
                 }
+                if (c + 1 < NCH)
+#pragma unroll
+                    for (int ar = 0; ar < (BLK ? 5 : 1); ar++) {
+                        const uint32_t* q = Db + (ibase + (c + 1) * R * pitch + toff[0]) + ar * pitch;
+                        dpa[ar] = *reinterpret_cast<const u4a4k*>(q);
+                        dpb[ar] = *reinterpret_cast<const u2a4k*>(q + 4);
+                    }
             } else if (ok) {
                 // LPP 64: the run's I bytes and derivative words of both tap rows, vector loads
                 uint64_t r0 = 0, r1 = 0;
@@ -862,7 +890,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
                 jsh = (uint32_t)(u & 3);
                 jb0 = reinterpret_cast<const uint8_t*>(u & ~(uintptr_t)3);
 #pragma unroll
-                for (int ar = 0; ar < (BLK ? 5 : 1); ar++) jr[ar] = *reinterpret_cast<const u3a4k*>(jb0 + ar * pitch);
+                for (int ar = 0; ar < (BLK ? 5 : 1); ar++) jr[ar] = gload<u3a4k>(reinterpret_cast<uintptr_t>(jb0 + ar * pitch));
             }
 #pragma unroll
             for (int c = 0; c < NCH; c++) {
@@ -899,7 +927,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LPP == 32 ? 
                     if (c + 1 < NCH)
 #pragma unroll
                         for (int ar = 0; ar < (BLK ? 5 : 1); ar++)
-                            jr[ar] = *reinterpret_cast<const u3a4k*>(jb0 + ((c + 1) * R + ar) * pitch);
+                            jr[ar] = gload<u3a4k>(reinterpret_cast<uintptr_t>(jb0 + ((c + 1) * R + ar) * pitch));
                 } else if (act) {
                     uint32_t j0l = 0, j0h = 0, j1l = 0, j1h = 0;
                     uint32_t j0w[RW > 0 ? RW : 1] = {}, j1w[RW > 0 ? RW : 1] = {};
