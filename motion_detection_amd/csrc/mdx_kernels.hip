@@ -1150,13 +1150,10 @@ __device__ double dev_hypot(double x, double y)
 // getPerspectiveTransform(src, dst) = solve(A, b, DECOMP_SVD) on the 8x8 DLT system:
 // lapack.cpp JacobiSVDImpl_<double> (one-sided Jacobi on A's columns, eps 10*DBL_EPSILON,
 // max(m,30) sweeps, descending sort) then SVBkSb (threshold 2*DBL_EPSILON*sum(w)).
-// The working arrays live in LDS (one lane runs the solve): as private arrays they were
-// scratch memory, whose latency every dependent step of the sweep paid.  Element e of the
-// working set is fw[e * S]: S = 1 for one lane (k_fit), S = lanes for a lane-interleaved set
-// (k_ransac_hyp: lane l's element e at fw[e * S + l], conflict-free across lanes).
-struct FitWork {
-    double At[64], Vt[64], W[8], bv[8], x[8];
-};
+// One lane runs this solve (k_ransac_hyp: one hypothesis per lane); its working arrays (At[64],
+// Vt[64], W[8], bv[8], x[8]) live in LDS, lane-interleaved: lane l's element e at fw[e * S + l]
+// (S = lanes, conflict-free across lanes).  As private arrays they were scratch memory.
+// k_fit / k_band_fit run the wave-parallel form below (dev_perspective_fit_wave).
 constexpr int kFitWorkDoubles = 152;
 template <int S>
 __device__ __forceinline__ void dev_perspective_fit_s(const float* src, const float* dst, double* M, double* fw)
@@ -1266,10 +1263,189 @@ __device__ __forceinline__ void dev_perspective_fit_s(const float* src, const fl
 #undef BV
 #undef XV
 }
-__device__ __forceinline__ void dev_perspective_fit(const float* src, const float* dst, double* M, FitWork& fw)
+// The same solve by one wave (k_fit, k_band_fit: every lane of a 64-lane workgroup calls it with
+// the same src / dst).  Each rotation, and every other step, computes what dev_perspective_fit_s
+// does in the same order within its column, so the result is bit-identical; what changes is that
+// rotations on disjoint column pairs run at once.  Rotation (i, j) of sweep s (r-th in the
+// reference's order) needs only the latest earlier rotations on columns i and j, which puts it at
+// dependency depth 8 s + d_r (d_r = 0..12): depth L holds sweep L/8's rotations at d = L%8 and
+// sweep L/8 - 1's at d = L%8 + 8, at most four, on disjoint columns (kJacSlot: i | j << 3 |
+// previous-sweep << 6).  A sweep is complete at depth 8 s + 12; if it changed nothing, the next
+// sweep's rotations already run saw the same columns and skipped too, so stopping there leaves the
+// reference's state.  One lane per rotation (lanes 0..3), one per column elsewhere (lanes 0..7).
+// fw: kFitWaveDoubles of LDS.  M: the 9 entries, in every lane.
+__constant__ uint8_t kJacSlot[8][4] = {{0x08, 0x7a, 0x73, 0x6c}, {0x10, 0x7b, 0x74, 0xff}, {0x18, 0x11, 0x7c, 0x75},
+                                       {0x20, 0x19, 0x7d, 0xff}, {0x28, 0x21, 0x1a, 0x7e}, {0x30, 0x29, 0x22, 0xff},
+                                       {0x38, 0x31, 0x2a, 0x23}, {0x39, 0x32, 0x2b, 0xff}};
+constexpr int kFitWaveDoubles = 168;   // At 64, Vt 64, W 8, b 8, s 8, use 8, x 8
+constexpr int kJacSweeps = 30;
+
+__device__ void dev_perspective_fit_wave(const float* src, const float* dst, double* M, double* fw)
 {
-    static_assert(sizeof(FitWork) == kFitWorkDoubles * sizeof(double), "FitWork layout");
-    dev_perspective_fit_s<1>(src, dst, M, reinterpret_cast<double*>(&fw));
+    double* At = fw;          // column c of A: At[c * 8 + k]
+    double* Vt = fw + 64;     // row c of Vt
+    double* W = fw + 128;
+    double* bv = fw + 136;
+    double* sv = fw + 144;    // back-substitution coefficient of row i
+    double* uv = fw + 152;    // 1: row i passes the threshold
+    double* xv = fw + 160;
+    const int lane = threadIdx.x & 63;
+    const double eps = DBL_EPSILON * 10;
+    if (lane == 0) {
+        for (int i = 0; i < 64; i++) At[i] = 0.0;
+        for (int i = 0; i < 4; i++) {
+            const float sx = src[2 * i], sy = src[2 * i + 1], dx = dst[2 * i], dy = dst[2 * i + 1];
+            At[0 * 8 + i] = sx; At[1 * 8 + i] = sy; At[2 * 8 + i] = 1.0;
+            At[3 * 8 + i + 4] = sx; At[4 * 8 + i + 4] = sy; At[5 * 8 + i + 4] = 1.0;
+            At[6 * 8 + i] = (double)(-sx * dx);
+            At[7 * 8 + i] = (double)(-sy * dx);
+            At[6 * 8 + i + 4] = (double)(-sx * dy);
+            At[7 * 8 + i + 4] = (double)(-sy * dy);
+            bv[i] = dx;
+            bv[i + 4] = dy;
+        }
+    }
+    __syncthreads();
+    if (lane < 8) {
+        double sd = 0;
+        for (int k = 0; k < 8; k++) { const double t = At[lane * 8 + k]; sd += t * t; }
+        W[lane] = sd;
+        for (int k = 0; k < 8; k++) Vt[lane * 8 + k] = k == lane ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    bool chg_prev = false, chg_cur = false;
+    for (int L = 0; L < 8 * (kJacSweeps - 1) + 13; L++) {
+        const int ph = L & 7, sweep = L >> 3;
+        bool rot = false, prev = false;
+        if (lane < 4) {
+            const int e = kJacSlot[ph][lane];
+            prev = (e >> 6) & 1;
+            const int s_of = sweep - (int)prev;
+            if (e != 0xff && s_of >= 0 && s_of < kJacSweeps) {
+                const int i = e & 7, j = (e >> 3) & 7;
+                double ai[8], aj[8], vi[8], vj[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    ai[k] = At[i * 8 + k]; aj[k] = At[j * 8 + k];
+                    vi[k] = Vt[i * 8 + k]; vj[k] = Vt[j * 8 + k];
+                }
+                double aa = W[i], p = 0, bb = W[j];
+#pragma unroll
+                for (int k = 0; k < 8; k++) p += ai[k] * aj[k];
+                if (!(fabs(p) <= eps * __builtin_sqrt(aa * bb))) {
+                    p *= 2;
+                    const double beta = aa - bb, gamma = dev_hypot(p, beta);
+                    double c, s;
+                    if (beta < 0) {
+                        const double delta = (gamma - beta) * 0.5;
+                        s = __builtin_sqrt(delta / gamma);
+                        c = p / (gamma * s * 2);
+                    } else {
+                        c = __builtin_sqrt((gamma + beta) / (gamma * 2));
+                        s = p / (gamma * c * 2);
+                    }
+                    aa = bb = 0;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        const double t0 = c * ai[k] + s * aj[k];
+                        const double t1 = -s * ai[k] + c * aj[k];
+                        At[i * 8 + k] = t0; At[j * 8 + k] = t1;
+                        aa += t0 * t0; bb += t1 * t1;
+                    }
+                    W[i] = aa; W[j] = bb;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        const double t0 = c * vi[k] + s * vj[k];
+                        const double t1 = -s * vi[k] + c * vj[k];
+                        Vt[i * 8 + k] = t0; Vt[j * 8 + k] = t1;
+                    }
+                    rot = true;
+                }
+            }
+        }
+        chg_prev = chg_prev || __ballot(rot && prev) != 0;
+        chg_cur = chg_cur || __ballot(rot && !prev) != 0;
+        __syncthreads();
+        if (ph == 4 && sweep >= 1 && !chg_prev) break;   // sweep - 1 complete, nothing changed
+        if (ph == 7) { chg_prev = chg_cur; chg_cur = false; }
+    }
+    // singular values = column norms; descending selection sort (the reference's comparisons, on
+    // every lane), applied as a permutation of the columns
+    double w[8];
+    int perm[8];
+    if (lane < 8) {
+        double sd = 0;
+        for (int k = 0; k < 8; k++) { const double t = At[lane * 8 + k]; sd += t * t; }
+        W[lane] = __builtin_sqrt(sd);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; i++) { w[i] = W[i]; perm[i] = i; }
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        int j = i;
+        double wj = w[i];
+#pragma unroll
+        for (int k = i + 1; k < 8; k++)
+            if (wj < w[k]) { j = k; wj = w[k]; }
+        int pj = perm[i];
+#pragma unroll
+        for (int k = i + 1; k < 8; k++)
+            if (k == j) pj = perm[k];
+#pragma unroll
+        for (int k = i + 1; k < 8; k++)
+            if (k == j) { w[k] = w[i]; perm[k] = perm[i]; }
+        w[i] = wj;
+        perm[i] = pj;
+    }
+    double a[8], v[8];
+    if (lane < 8) {
+        int src_c = perm[0];
+#pragma unroll
+        for (int k = 1; k < 8; k++) if (lane == k) src_c = perm[k];
+#pragma unroll
+        for (int k = 0; k < 8; k++) { a[k] = At[src_c * 8 + k]; v[k] = Vt[src_c * 8 + k]; }
+    }
+    __syncthreads();
+    double threshold = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) threshold += w[i];
+    threshold *= DBL_EPSILON * 2;
+    if (lane < 8) {
+        double wl = w[0];
+#pragma unroll
+        for (int k = 1; k < 8; k++) if (lane == k) wl = w[k];
+        // left singular vectors (rows with W <= DBL_MIN fail the threshold below anyway)
+        if (!(wl <= DBL_MIN)) {
+            const double s = 1 / wl;
+#pragma unroll
+            for (int k = 0; k < 8; k++) a[k] *= s;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) Vt[lane * 8 + k] = v[k];
+        const bool use = !(fabs(wl) <= threshold);
+        double s = 0;
+        if (use) {
+            const double wi = 1 / wl;
+#pragma unroll
+            for (int k = 0; k < 8; k++) s += a[k] * bv[k];
+            s *= wi;
+        }
+        sv[lane] = s;
+        uv[lane] = use ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (lane < 8) {
+        double x = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            if (uv[i] != 0.0) x = x + sv[i] * Vt[i * 8 + lane];
+        xv[lane] = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; i++) M[i] = xv[i];
+    M[8] = 1.;
 }
 
 // lapack.cpp invert(DECOMP_LU) for 3x3 CV_64F: cofactors times 1/det3; det == 0 -> zeros.
@@ -1380,18 +1556,11 @@ __global__ __launch_bounds__(64) void k_fit(const float* __restrict__ next_pts, 
         }
         carry += __shfl(incl, 63);
     }
-    if (lane != 0) return;
-    __shared__ FitWork fw;
+    // carry and pick are wave-uniform: the whole wave runs the fit, lane 0 writes the record
+    __shared__ double fw[kFitWaveDoubles];
     PairFit& f = fits[pair];
     const int total = carry;
-    f.num_vectors = total;
-    if (fit_mode == MDX_FIT_EXTERNAL) {
-        for (int k = 0; k < 9; k++) f.H[k] = H_ext[(long long)pair * 9 + k];
-        dev_invert3x3(f.H, f.Hinv);
-        f.fit_status = 0;
-    } else if (fit_mode == MDX_FIT_RANSAC && total >= 4) {
-        f.fit_status = 0;                        // H / Hinv: k_ransac_pick
-    } else if (total >= 4) {
+    if (fit_mode != MDX_FIT_EXTERNAL && fit_mode != MDX_FIT_RANSAC && total >= 4) {
         float src[8], dst[8];
         for (int r = 0; r < 4; r++) {
             const int i = pick[r];
@@ -1401,9 +1570,23 @@ __global__ __launch_bounds__(64) void k_fit(const float* __restrict__ next_pts, 
             dst[2 * r] = e.x;
             dst[2 * r + 1] = e.y;
         }
-        dev_perspective_fit(src, dst, f.H, fw);
+        double H[9];
+        dev_perspective_fit_wave(src, dst, H, fw);
+        if (lane != 0) return;
+        for (int k = 0; k < 9; k++) f.H[k] = H[k];
+        dev_invert3x3(H, f.Hinv);
+        f.fit_status = 0;
+        f.num_vectors = total;
+        return;
+    }
+    if (lane != 0) return;
+    f.num_vectors = total;
+    if (fit_mode == MDX_FIT_EXTERNAL) {
+        for (int k = 0; k < 9; k++) f.H[k] = H_ext[(long long)pair * 9 + k];
         dev_invert3x3(f.H, f.Hinv);
         f.fit_status = 0;
+    } else if (fit_mode == MDX_FIT_RANSAC && total >= 4) {
+        f.fit_status = 0;                        // H / Hinv: k_ransac_pick
     } else {
         for (int k = 0; k < 9; k++) { f.H[k] = 0.0; f.Hinv[k] = 0.0; }
         f.fit_status = total == 0 ? 1 : 2;
@@ -1654,10 +1837,10 @@ __device__ void band_source_rows(const double* M, int w, int h, int y0, int y1, 
     if (r1 < r0) r1 = r0;
 }
 
-__global__ void k_band_fit(const mdx_band_cand* __restrict__ cands, int nrec, PairFit* __restrict__ fit, int w, int h,
-                           int y0, int y1)
+__global__ __launch_bounds__(64) void k_band_fit(const mdx_band_cand* __restrict__ cands, int nrec,
+                                                 PairFit* __restrict__ fit, int w, int h, int y0, int y1)
 {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    // every lane merges the records (uniform loads), the wave runs the fit, lane 0 writes
     int total = 0;
     int best[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};
     float bs[8] = {}, bd[8] = {};
@@ -1678,14 +1861,19 @@ __global__ void k_band_fit(const mdx_band_cand* __restrict__ cands, int nrec, Pa
         }
     }
     PairFit& f = *fit;
-    f.num_vectors = total;
-    __shared__ FitWork fw;
+    __shared__ double fw[kFitWaveDoubles];
     if (total >= 4) {
-        dev_perspective_fit(bs, bd, f.H, fw);
-        dev_invert3x3(f.H, f.Hinv);
+        double H[9];
+        dev_perspective_fit_wave(bs, bd, H, fw);
+        if (threadIdx.x != 0) return;
+        f.num_vectors = total;
+        for (int k = 0; k < 9; k++) f.H[k] = H[k];
+        dev_invert3x3(H, f.Hinv);
         f.fit_status = 0;
         band_source_rows(f.Hinv, w, h, y0, y1, f.src_y0, f.src_y1);
     } else {
+        if (threadIdx.x != 0) return;
+        f.num_vectors = total;
         for (int k = 0; k < 9; k++) { f.H[k] = 0.0; f.Hinv[k] = 0.0; }
         f.fit_status = total == 0 ? 1 : 2;
         f.src_y0 = f.src_y1 = 0;   // no warp (zero mask)
