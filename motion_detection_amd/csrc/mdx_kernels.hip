@@ -1265,42 +1265,70 @@ __device__ __forceinline__ void dev_perspective_fit_s(const float* src, const fl
 }
 // The same solve by one wave (k_fit, k_band_fit: every lane of a 64-lane workgroup calls it with
 // the same src / dst).  Each rotation, and every other step, computes what dev_perspective_fit_s
-// does in the same order within its column, so the result is bit-identical; what changes is that
-// rotations on disjoint column pairs run at once.  Rotation (i, j) of sweep s (r-th in the
-// reference's order) needs only the latest earlier rotations on columns i and j, which puts it at
-// dependency depth 8 s + d_r (d_r = 0..12): depth L holds sweep L/8's rotations at d = L%8 and
-// sweep L/8 - 1's at d = L%8 + 8, at most four, on disjoint columns (kJacSlot: i | j << 3 |
-// previous-sweep << 6).  A sweep is complete at depth 8 s + 12; if it changed nothing, the next
-// sweep's rotations already run saw the same columns and skipped too, so stopping there leaves the
-// reference's state.  One lane per rotation (lanes 0..3), one per column elsewhere (lanes 0..7).
-// fw: kFitWaveDoubles of LDS.  M: the 9 entries, in every lane.
+// does, in the same order within each sum, so the result is bit-identical; what changes is the
+// schedule.  Rotation (i, j) of sweep s (r-th in the reference's order) needs only the latest
+// earlier rotations on columns i and j, which puts it at dependency depth 8 s + d_r (d_r = 0..12):
+// depth L holds sweep L/8's rotations at d = L%8 and sweep L/8 - 1's at d = L%8 + 8, at most four,
+// on disjoint columns (kJacSlot: i | j << 3 | previous-sweep << 6).  A sweep is complete at depth
+// 8 s + 12; if it changed nothing, the next sweep's rotations already run saw the same columns and
+// skipped too, so stopping there leaves the reference's state.
+// Element-parallel rotations: slot q of a depth runs on the 16-lane DPP row q, lane e holding
+// element e of A's column (e < 8) or element e - 8 of Vt's row (e >= 8) for both columns, so the
+// update is one step; the 8-term dot products (p, and the new column norms) are summed in the
+// reference's order from row_newbcast broadcasts of lanes 0..7 (v_mov_b64 DPP, then the add), and
+// the scalar part (hypot, square roots, divisions) runs once per row.  The column-wise steps after
+// the sweeps run one lane per column.  fw: kFitWaveDoubles of LDS.  M: the 9 entries, in every lane.
 __constant__ uint8_t kJacSlot[8][4] = {{0x08, 0x7a, 0x73, 0x6c}, {0x10, 0x7b, 0x74, 0xff}, {0x18, 0x11, 0x7c, 0x75},
                                        {0x20, 0x19, 0x7d, 0xff}, {0x28, 0x21, 0x1a, 0x7e}, {0x30, 0x29, 0x22, 0xff},
                                        {0x38, 0x31, 0x2a, 0x23}, {0x39, 0x32, 0x2b, 0xff}};
-constexpr int kFitWaveDoubles = 168;   // At 64, Vt 64, W 8, b 8, s 8, use 8, x 8
+constexpr int kFitWaveDoubles = 168;   // X 8 x 16 (A column | Vt row), W 8, b 8, s 8, use 8, x 8
 constexpr int kJacSweeps = 30;
+
+// lane T of this lane's 16-lane row (s_nop: the DPP source may have been written by the previous VALU op)
+#define MDX_ROWB(T)                                                                                      \
+    __device__ __forceinline__ double rowb##T(double v)                                                  \
+    {                                                                                                    \
+        double r;                                                                                        \
+        asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:" #T " row_mask:0xf bank_mask:0xf"  \
+                     : "=v"(r) : "v"(v));                                                                \
+        return r;                                                                                        \
+    }
+MDX_ROWB(0) MDX_ROWB(1) MDX_ROWB(2) MDX_ROWB(3) MDX_ROWB(4) MDX_ROWB(5) MDX_ROWB(6) MDX_ROWB(7)
+#undef MDX_ROWB
+// ((((0 + v0) + v1) + ...) + v7) over lanes 0..7 of the row: a column's sum in the reference's order
+__device__ __forceinline__ double rowsum8(double v)
+{
+    double s = 0.0;
+    s = s + rowb0(v); s = s + rowb1(v); s = s + rowb2(v); s = s + rowb3(v);
+    s = s + rowb4(v); s = s + rowb5(v); s = s + rowb6(v); s = s + rowb7(v);
+    return s;
+}
 
 __device__ void dev_perspective_fit_wave(const float* src, const float* dst, double* M, double* fw)
 {
-    double* At = fw;          // column c of A: At[c * 8 + k]
-    double* Vt = fw + 64;     // row c of Vt
+    double* X = fw;           // X[c * 16 + k]: A[k][c] (k < 8), Vt[c][k - 8] (k >= 8)
     double* W = fw + 128;
     double* bv = fw + 136;
     double* sv = fw + 144;    // back-substitution coefficient of row i
     double* uv = fw + 152;    // 1: row i passes the threshold
     double* xv = fw + 160;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, q = lane >> 4, e = lane & 15;
     const double eps = DBL_EPSILON * 10;
+    if (lane < 8) {
+        const int c = lane;
+        for (int k = 0; k < 16; k++) X[c * 16 + k] = k == 8 + c ? 1.0 : 0.0;
+    }
+    __syncthreads();
     if (lane == 0) {
-        for (int i = 0; i < 64; i++) At[i] = 0.0;
         for (int i = 0; i < 4; i++) {
             const float sx = src[2 * i], sy = src[2 * i + 1], dx = dst[2 * i], dy = dst[2 * i + 1];
-            At[0 * 8 + i] = sx; At[1 * 8 + i] = sy; At[2 * 8 + i] = 1.0;
-            At[3 * 8 + i + 4] = sx; At[4 * 8 + i + 4] = sy; At[5 * 8 + i + 4] = 1.0;
-            At[6 * 8 + i] = (double)(-sx * dx);
-            At[7 * 8 + i] = (double)(-sy * dx);
-            At[6 * 8 + i + 4] = (double)(-sx * dy);
-            At[7 * 8 + i + 4] = (double)(-sy * dy);
+            // A[i][c] at X[c * 16 + i]; rows i (x equations) and i + 4 (y equations)
+            X[0 * 16 + i] = sx; X[1 * 16 + i] = sy; X[2 * 16 + i] = 1.0;
+            X[3 * 16 + i + 4] = sx; X[4 * 16 + i + 4] = sy; X[5 * 16 + i + 4] = 1.0;
+            X[6 * 16 + i] = (double)(-sx * dx);
+            X[7 * 16 + i] = (double)(-sy * dx);
+            X[6 * 16 + i + 4] = (double)(-sx * dy);
+            X[7 * 16 + i + 4] = (double)(-sy * dy);
             bv[i] = dx;
             bv[i + 4] = dy;
         }
@@ -1308,59 +1336,44 @@ __device__ void dev_perspective_fit_wave(const float* src, const float* dst, dou
     __syncthreads();
     if (lane < 8) {
         double sd = 0;
-        for (int k = 0; k < 8; k++) { const double t = At[lane * 8 + k]; sd += t * t; }
+        for (int k = 0; k < 8; k++) { const double t = X[lane * 16 + k]; sd += t * t; }
         W[lane] = sd;
-        for (int k = 0; k < 8; k++) Vt[lane * 8 + k] = k == lane ? 1.0 : 0.0;
     }
     __syncthreads();
     bool chg_prev = false, chg_cur = false;
     for (int L = 0; L < 8 * (kJacSweeps - 1) + 13; L++) {
         const int ph = L & 7, sweep = L >> 3;
-        bool rot = false, prev = false;
-        if (lane < 4) {
-            const int e = kJacSlot[ph][lane];
-            prev = (e >> 6) & 1;
-            const int s_of = sweep - (int)prev;
-            if (e != 0xff && s_of >= 0 && s_of < kJacSweeps) {
-                const int i = e & 7, j = (e >> 3) & 7;
-                double ai[8], aj[8], vi[8], vj[8];
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    ai[k] = At[i * 8 + k]; aj[k] = At[j * 8 + k];
-                    vi[k] = Vt[i * 8 + k]; vj[k] = Vt[j * 8 + k];
+        const int ent = kJacSlot[ph][q];
+        const bool prev = (ent >> 6) & 1;
+        const int s_of = sweep - (int)prev;
+        bool rot = false;
+        if (ent != 0xff && s_of >= 0 && s_of < kJacSweeps) {   // uniform over the row
+            const int i = ent & 7, j = (ent >> 3) & 7;
+            const double xi = X[i * 16 + e], xj = X[j * 16 + e];
+            const double aa0 = W[i], bb0 = W[j];
+            double p = rowsum8(xi * xj);
+            if (!(fabs(p) <= eps * __builtin_sqrt(aa0 * bb0))) {   // uniform over the row
+                p *= 2;
+                const double beta = aa0 - bb0, gamma = dev_hypot(p, beta);
+                double c, s;
+                if (beta < 0) {
+                    const double delta = (gamma - beta) * 0.5;
+                    s = __builtin_sqrt(delta / gamma);
+                    c = p / (gamma * s * 2);
+                } else {
+                    c = __builtin_sqrt((gamma + beta) / (gamma * 2));
+                    s = p / (gamma * c * 2);
                 }
-                double aa = W[i], p = 0, bb = W[j];
-#pragma unroll
-                for (int k = 0; k < 8; k++) p += ai[k] * aj[k];
-                if (!(fabs(p) <= eps * __builtin_sqrt(aa * bb))) {
-                    p *= 2;
-                    const double beta = aa - bb, gamma = dev_hypot(p, beta);
-                    double c, s;
-                    if (beta < 0) {
-                        const double delta = (gamma - beta) * 0.5;
-                        s = __builtin_sqrt(delta / gamma);
-                        c = p / (gamma * s * 2);
-                    } else {
-                        c = __builtin_sqrt((gamma + beta) / (gamma * 2));
-                        s = p / (gamma * c * 2);
-                    }
-                    aa = bb = 0;
-#pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        const double t0 = c * ai[k] + s * aj[k];
-                        const double t1 = -s * ai[k] + c * aj[k];
-                        At[i * 8 + k] = t0; At[j * 8 + k] = t1;
-                        aa += t0 * t0; bb += t1 * t1;
-                    }
-                    W[i] = aa; W[j] = bb;
-#pragma unroll
-                    for (int k = 0; k < 8; k++) {
-                        const double t0 = c * vi[k] + s * vj[k];
-                        const double t1 = -s * vi[k] + c * vj[k];
-                        Vt[i * 8 + k] = t0; Vt[j * 8 + k] = t1;
-                    }
-                    rot = true;
+                const double t0 = c * xi + s * xj;
+                const double t1 = -s * xi + c * xj;
+                X[i * 16 + e] = t0;
+                X[j * 16 + e] = t1;
+                const double aa = rowsum8(t0 * t0), bb = rowsum8(t1 * t1);
+                if (e == 0) {
+                    W[i] = aa;
+                    W[j] = bb;
                 }
+                rot = true;
             }
         }
         chg_prev = chg_prev || __ballot(rot && prev) != 0;
@@ -1375,7 +1388,7 @@ __device__ void dev_perspective_fit_wave(const float* src, const float* dst, dou
     int perm[8];
     if (lane < 8) {
         double sd = 0;
-        for (int k = 0; k < 8; k++) { const double t = At[lane * 8 + k]; sd += t * t; }
+        for (int k = 0; k < 8; k++) { const double t = X[lane * 16 + k]; sd += t * t; }
         W[lane] = __builtin_sqrt(sd);
     }
     __syncthreads();
@@ -1404,7 +1417,7 @@ __device__ void dev_perspective_fit_wave(const float* src, const float* dst, dou
 #pragma unroll
         for (int k = 1; k < 8; k++) if (lane == k) src_c = perm[k];
 #pragma unroll
-        for (int k = 0; k < 8; k++) { a[k] = At[src_c * 8 + k]; v[k] = Vt[src_c * 8 + k]; }
+        for (int k = 0; k < 8; k++) { a[k] = X[src_c * 16 + k]; v[k] = X[src_c * 16 + 8 + k]; }
     }
     __syncthreads();
     double threshold = 0;
@@ -1422,7 +1435,7 @@ __device__ void dev_perspective_fit_wave(const float* src, const float* dst, dou
             for (int k = 0; k < 8; k++) a[k] *= s;
         }
 #pragma unroll
-        for (int k = 0; k < 8; k++) Vt[lane * 8 + k] = v[k];
+        for (int k = 0; k < 8; k++) X[lane * 16 + 8 + k] = v[k];
         const bool use = !(fabs(wl) <= threshold);
         double s = 0;
         if (use) {
@@ -1439,7 +1452,7 @@ __device__ void dev_perspective_fit_wave(const float* src, const float* dst, dou
         double x = 0;
 #pragma unroll
         for (int i = 0; i < 8; i++)
-            if (uv[i] != 0.0) x = x + sv[i] * Vt[i * 8 + lane];
+            if (uv[i] != 0.0) x = x + sv[i] * X[i * 16 + 8 + lane];
         xv[lane] = x;
     }
     __syncthreads();
