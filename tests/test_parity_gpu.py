@@ -294,6 +294,63 @@ def test_row_tiled_matches_full(mdx, monkeypatch, w, h, ps, nb, ch, pipe):
     assert int((out["mask"] != full.mask).sum()) == 0
 
 
+def _fit_cases(n, seed):
+    """First-4 correspondences for the fit alone: random quads, one grid column (the typical first-4
+    pick, collinear sources), a repeated point, all-zero destinations, 8K-scale coordinates."""
+    rng = np.random.default_rng(seed)
+    src = np.empty((n, 4, 2), np.float32)
+    dst = np.empty((n, 4, 2), np.float32)
+    for c in range(n):
+        kind = c % 5
+        scale = 7680 if kind == 4 else 1920
+        s = (10 * rng.integers(0, scale // 10, (4, 2))).astype(np.float32)
+        if kind == 1:
+            s[:, 0] = s[0, 0]
+            s[:, 1] = 10 * rng.integers(0, 100) + 10 * np.arange(4)
+        if kind == 2:
+            s[3] = s[0]
+        d = (s + rng.uniform(-3, 3, (4, 2))).astype(np.float32)
+        if kind == 3:
+            d[:] = 0
+        src[c], dst[c] = s, d
+    return src, dst
+
+
+def test_fit_arbitrary_correspondences(mdx, oracle):
+    """k_band_fit's wave-parallel JacobiSVD fit (the same solve as k_fit) on 250 arbitrary
+    first-4 correspondences, fed through the band API's records: H equals the oracle's
+    getPerspectiveTransform bit for bit, degenerate inputs included (collinear, repeated, zero)."""
+    from motion_detection_amd import rowtile
+    w, h, ps, n = 320, 240, 10, 250
+    src, dst = _fit_cases(n, 20261018)
+    a, b, _ = mdx.synth_pair(9, w, h, 1)
+    npts = mdx.grid_count(w, h, ps)
+    recs = np.zeros(n, rowtile.BAND_CAND_DTYPE)
+    recs["count"] = 4
+    recs["n"] = 4
+    recs["idx"] = np.arange(4)
+    recs["src"] = src.reshape(n, 8)
+    recs["dst"] = dst.reshape(n, 8)
+    with mdx.Context(0, w, h, 1, pixel_step=ps, min_vector_size=1.0) as c:
+        d = {k: c.dev_alloc(sz) for k, sz in dict(i1=a.nbytes, i2=b.nbytes, np=npts * 8, st=npts, cand=96,
+                                                   cands=n * 96, mask=w * h, H=n * 72).items()}
+        try:
+            c.h2d(d["i1"], a); c.h2d(d["i2"], b)
+            c.band_flow_dev(d["i1"], d["i2"], w, h, w, mdx.FMT_GRAY8, 0, h, d["np"], d["st"], d["cand"])
+            c.h2d(d["cands"], recs)
+            for i in range(n):        # record i alone: its four points are the first four overall
+                c.band_fit_warp_dev(1, d["cands"] + 96 * i, 0, h, d["mask"], d["H"] + 72 * i)
+            c.sync()
+            H = np.empty((n, 9))
+            c.d2h(H, d["H"])
+        finally:
+            for p in d.values():
+                c.dev_free(p)
+    bad = [i for i in range(n)
+           if not np.array_equal(H[i].view(np.uint64), oracle.get_perspective_transform(src[i], dst[i]).ravel().view(np.uint64))]
+    assert not bad, f"{len(bad)} of {n} fits differ, first {bad[:5]}"
+
+
 @pytest.mark.parametrize("B,uniq,pipe", [(2, 2, 0), (8, 4, 1)])
 def test_full_path_4k_bit_exact(mdx, oracle, B, uniq, pipe):
     """Config C2 (3840x2160, 5 pyramid levels) through the batched device entry: every output
