@@ -1284,23 +1284,27 @@ __constant__ uint8_t kJacSlot[8][4] = {{0x08, 0x7a, 0x73, 0x6c}, {0x10, 0x7b, 0x
 constexpr int kFitWaveDoubles = 168;   // X 8 x 16 (A column | Vt row), W 8, b 8, s 8, use 8, x 8
 constexpr int kJacSweeps = 30;
 
-// lane T of this lane's 16-lane row (s_nop: the DPP source may have been written by the previous VALU op)
-#define MDX_ROWB(T)                                                                                      \
-    __device__ __forceinline__ double rowb##T(double v)                                                  \
-    {                                                                                                    \
-        double r;                                                                                        \
-        asm volatile("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:" #T " row_mask:0xf bank_mask:0xf"  \
-                     : "=v"(r) : "v"(v));                                                                \
-        return r;                                                                                        \
-    }
-MDX_ROWB(0) MDX_ROWB(1) MDX_ROWB(2) MDX_ROWB(3) MDX_ROWB(4) MDX_ROWB(5) MDX_ROWB(6) MDX_ROWB(7)
-#undef MDX_ROWB
-// ((((0 + v0) + v1) + ...) + v7) over lanes 0..7 of the row: a column's sum in the reference's order
+// ((((0 + v0) + v1) + ...) + v7) over lanes 0..7 of the lane's 16-lane DPP row: a column's sum in the
+// reference's order.  The eight broadcasts (v_mov_b64 row_newbcast; v_add_f64 has no DPP form on
+// gfx950) in one block behind s_nop 4: five wait states cover both DPP hazards, a VALU write of the
+// source VGPR (two) and of EXEC (five), whatever the compiler schedules before the block.
 __device__ __forceinline__ double rowsum8(double v)
 {
+    double b0, b1, b2, b3, b4, b5, b6, b7;
+    asm volatile("s_nop 4\n\t"
+                 "v_mov_b64_dpp %0, %8 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_mov_b64_dpp %1, %8 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_mov_b64_dpp %2, %8 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_mov_b64_dpp %3, %8 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_mov_b64_dpp %4, %8 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_mov_b64_dpp %5, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_mov_b64_dpp %6, %8 row_newbcast:6 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_mov_b64_dpp %7, %8 row_newbcast:7 row_mask:0xf bank_mask:0xf"
+                 : "=&v"(b0), "=&v"(b1), "=&v"(b2), "=&v"(b3), "=&v"(b4), "=&v"(b5), "=&v"(b6), "=&v"(b7)
+                 : "v"(v));
     double s = 0.0;
-    s = s + rowb0(v); s = s + rowb1(v); s = s + rowb2(v); s = s + rowb3(v);
-    s = s + rowb4(v); s = s + rowb5(v); s = s + rowb6(v); s = s + rowb7(v);
+    s = s + b0; s = s + b1; s = s + b2; s = s + b3;
+    s = s + b4; s = s + b5; s = s + b6; s = s + b7;
     return s;
 }
 
